@@ -1,0 +1,56 @@
+"""Helpers to load the golden fixtures recorded from the reference (tests/golden/gen_golden.py)."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+import numpy as np
+import torch
+
+from count_pipnet_amd.synthetic import synth_exponential, synth_images, synth_tensor
+
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz"))
+
+
+def load_golden(name: str):
+    z = np.load(os.path.join(GOLDEN_DIR, name + ".npz"), allow_pickle=False)
+    rec = {k: z[k] for k in z.files}
+    meta = json.loads(str(rec.pop("meta")))
+    return meta, rec
+
+
+def golden_args(meta) -> argparse.Namespace:
+    case = meta["case"]
+    a = dict(disable_pretrained=True, positive_grad_strategy=None, backward_clamp_strategy="Gated")
+    a.update({k: v for k, v in case.items() if k not in ("model", "num_classes", "batch", "size", "seed")})
+    return argparse.Namespace(**a)
+
+
+def golden_state_dict(meta):
+    return {k: synth_tensor(k, tuple(s), meta["case"]["seed"], meta["profile"]) for k, s in meta["keys"]}
+
+
+def golden_inputs(meta):
+    c = meta["case"]
+    xs = synth_images(c["batch"], c["size"], seed=c["seed"])
+    assert abs(float(xs.double().sum()) - meta["input_sum"]) < 1e-6 * max(1.0, meta["input_abs"]), \
+        "synthetic input generator drifted from the recorded fixture"
+    return xs
+
+
+def golden_noise(meta, shape):
+    return synth_exponential(tuple(shape), meta["noise_seed"])
+
+
+def proto_shape(meta, rec):
+    c = meta["case"]
+    p = rec["inf_pooled"].shape[1]
+    if "inf_proto" in rec:
+        return tuple(rec["inf_proto"].shape)
+    hw = rec["inf_proto_pixmax"].shape[1:]
+    return (c["batch"], p) + tuple(hw)
