@@ -1,0 +1,204 @@
+"""Throughput of the MI355X PIP-Net inference path (BASELINE.json metric).
+
+A "step" = one ``PIPNet.forward(xs, inference=True)`` of ConvNeXt-tiny-26 over one batch of
+64 synthetic 224x224 images per GPU (CUB-200 shape, 200 classes, fp32), inputs resident in
+HBM, plus -- for N > 1 -- the RCCL all-gather of logits and pooled presence over xGMI that
+replaces nn.DataParallel's gather (main.py:118).  Weak scaling: 64 images per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints one JSON line on rank 0 (fields described in DESIGN.md section "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec fwd, CUB-200 224×224 bs=64 ConvNeXt-tiny, 1/2/4/8 MI355X"
+PEAK_F32_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
+PEAK_HBM_GBS = 8000.0
+
+
+def make_net(device, num_classes=200):
+    from count_pipnet_amd.pipnet import get_pipnet
+    from count_pipnet_amd.synthetic import fill_module_
+    args = argparse.Namespace(net="convnext_tiny_26", disable_pretrained=True, num_features=0, bias=False)
+    with contextlib.redirect_stdout(io.StringIO()):
+        net, _ = get_pipnet(num_classes, args)
+    fill_module_(net, 21, "trained")
+    return net.eval().to(device), args
+
+
+class GemmTimer:
+    """Brackets every MFMA GEMM launch with HIP events on the launching stream."""
+
+    def __init__(self):
+        self.rec = []
+        self.enabled = False
+
+    def __call__(self, kname, flops, fn):
+        if not self.enabled:
+            fn()
+            return
+        s = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        fn()
+        e1.record(s)
+        self.rec.append((kname, flops, e0, e1))
+
+    def summary(self):
+        agg = {}
+        for kname, flops, e0, e1 in self.rec:
+            a = agg.setdefault(kname, [0, 0.0, 0.0])
+            a[0] += 1
+            a[1] += flops
+            a[2] += e0.elapsed_time(e1) * 1e-3
+        return agg
+
+
+def cpu_baseline(batch=4, min_seconds=10.0):
+    """The oracle (pure-torch CPU restatement of the reference forward) on the host cores."""
+    from oracle import ref_cpu
+    from count_pipnet_amd.synthetic import synth_images
+    net, args = make_net(torch.device("cpu"))
+    sd = {k: v for k, v in net.state_dict().items()}
+    xs = synth_images(batch, 224, seed=1)
+    with torch.no_grad():
+        ref_cpu.pipnet_forward(xs[:1], sd, args, inference=True)       # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            ref_cpu.pipnet_forward(xs, sd, args, inference=True)
+            n += batch
+            el = time.perf_counter() - t0
+            if el >= min_seconds:
+                break
+    return {"value": n / el, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} images (batches of {batch}, 224x224, ConvNeXt-tiny-26 PIP-Net fp32) in {el:.1f} s, "
+                      f"oracle/ref_cpu.py pipnet_forward on {torch.get_num_threads()} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from count_pipnet_amd import build, kernels
+    build.build()
+    from count_pipnet_amd.synthetic import synth_images
+    net, _ = make_net(dev)
+    xs = synth_images(a.batch, 224, seed=100 + rank).to(dev)
+    gather_out = [torch.empty(a.batch, 200, device=dev) for _ in range(world)]
+    gather_pooled = [torch.empty(a.batch, 768, device=dev) for _ in range(world)]
+
+    def step():
+        with torch.no_grad():
+            _, pooled, out = net(xs, inference=True)
+            if world > 1:
+                dist.all_gather(gather_out, out)
+                dist.all_gather(gather_pooled, pooled)
+        return out
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        step()
+    # dominant-kernel roofline: inside the timed region every MFMA GEMM launch is bracketed
+    # by HIP events recorded on the stream it is launched on (torch's current stream).
+    timer = GemmTimer()
+    kernels.set_launch_hook(timer)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    timer.enabled = False
+    kernels.set_launch_hook(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    agg = timer.summary()
+    dom = max(agg, key=lambda k: agg[k][2])
+    n_l, fl, tt = agg[dom]
+    gemm_flops = sum(v[1] for v in agg.values())
+    gemm_time = sum(v[2] for v in agg.values())
+
+    imgs = a.batch * world * a.steps
+    ms = elapsed / a.steps * 1e3
+    gflop_img = 40.094159616       # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
+    result = {
+        "metric": METRIC,
+        "value": imgs / elapsed,
+        "unit": "images/sec",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": "PIP-Net ConvNeXt-tiny-26 forward(inference=True), 224x224, 200 classes, fp32 "
+                               "(BASELINE configs[1]; configs[3] at N=8)",
+                   "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
+                   "parallelism": f"dp{world}", "exchange": "rccl all_gather(logits, pooled)" if world > 1 else None},
+        "roofline": {"bound": "mfma", "kernel": f"(anonymous namespace)::gemm_f32_tn_kernel<{dom[19:-1]}>",
+                     "achieved": fl / tt / 1e12, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": fl / tt / 1e12 / PEAK_F32_TFLOPS, "traffic": None,
+                     "launches_per_step": n_l / a.steps, "avg_launch_us": tt / n_l * 1e6,
+                     "algorithmic_gflop_per_launch": fl / n_l / 1e9},
+        "model_tflops": gflop_img * a.batch * world / (ms * 1e-3) / 1e3 / world,
+        "model_frac_of_f32_peak": gflop_img * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,
+        "gemm_all": {"tflops": gemm_flops / gemm_time / 1e12, "ms_per_step": gemm_time / a.steps * 1e3},
+    }
+    traffic_path = os.path.join(REPO, "profiles", "traffic_latest.json")
+    if os.path.exists(traffic_path):
+        with open(traffic_path) as f:
+            tr = json.load(f)
+        if tr.get("kernel_key") == dom:
+            result["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(min_seconds=a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,74 @@
+"""ctypes binding of the C-ABI in ``include/pipnet_amd.h`` (``libpipnet_amd.so``).
+
+This is exactly the binding a maintainer would add to the reference:
+the library takes raw device pointers, sizes and a hipStream_t, and returns a status
+code that is raised here as ``RuntimeError`` (the reference raises Python exceptions,
+SURVEY.md 8b).  There is no fallback: if the library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpipnet_amd.so")
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F32 = ctypes.c_float
+
+# name -> argtypes (restype is int status unless listed in _RESTYPE)
+SIGNATURES = {
+    "pipnet_amd_abi_version": [],
+    "pipnet_amd_status_string": [I32],
+    "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
+    "pipnet_conv2x2_f32": [P, I32, I32, I32, I32, P, P, I32, I32, P, P],
+    "pipnet_convnext_stem_f32": [P, I32, I32, I32, P, P, P, P, P, P],
+    "pipnet_dwconv7_ln_f32": [P, I32, I32, I32, I32, P, P, P, P, P, P],
+    "pipnet_layernorm_f32": [P, I64, I32, P, P, P, P],
+    "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],
+    "pipnet_nonneg_linear_f32": [P, I32, I32, P, P, I32, I32, F32, P, P, P],
+    "pipnet_count_gumbel_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
+    "pipnet_count_finish_f32": [P, P, I32, I32, I32, I32, P, P, P],
+    "pipnet_count_encode_f32": [P, I32, I32, I32, I32, I32, P, P, P],
+}
+_RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p}
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL = 0, 1, 2, 3, 4
+
+_lib = None
+
+
+class PipnetLibraryError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise if it is absent or incomplete."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PipnetLibraryError(
+            f"{LIB_PATH} is missing: the MI355X inference path has no fallback. "
+            "Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `python count_pipnet_amd/build.py`.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)          # AttributeError = missing export = loud failure
+        fn.argtypes = args
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().pipnet_amd_status_string(status).decode()
+        raise RuntimeError(f"{what} failed: PIPNET status {status} ({msg})")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)

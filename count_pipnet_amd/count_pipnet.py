@@ -1,0 +1,219 @@
+"""CountPIPNet -- drop-in for ``pipnet/count_pipnet.py`` (model, NonNegLinear, factory).
+
+``CountPIPNet.forward(xs, inference=False) -> (proto_features, counts | clamped_counts, out)``
+keeps the reference signature, attributes (``_max_count`` is the "is count net" probe of
+``pipnet/test.py:27``) and ``state_dict`` keys.  Eval + no-grad runs on HIP kernels:
+
+  backbone (NHWC) -> 1x1 add-on (MFMA) -> fused hard Gumbel-softmax + per-prototype count
+  (Philox4x32 Exp(1) noise in-kernel, or an injected draw) -> round / clamp ->
+  intermediate (identity / one-hot / linear / linear_full / bilinear on MFMA) -> NonNegLinear.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _lib
+from . import kernels as K
+from .backend import use_hip
+from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
+from .count_pipnet_utils import (BilinearIntermediate, ClampSTE, GumbelSoftmax, IdentityIntermediate,
+                                 LinearFull, LinearIntermediate, OneHotEncoder, STE_Round)
+from .pipnet import add_on_logits_hip
+
+
+class CountPIPNet(nn.Module):
+    """count_pipnet.py:14-168."""
+
+    def __init__(self, num_classes: int, num_prototypes: int, feature_net: nn.Module, args: argparse.Namespace,
+                 add_on_layers: nn.Module, intermediate_layer: nn.Module, classification_layer: nn.Module,
+                 max_count: int = 3, use_ste: bool = True, backward_clamp_strategy: str = "Identity"):
+        super().__init__()
+        assert num_classes > 0
+        self._num_features = args.num_features
+        self._num_classes = num_classes
+        self._num_prototypes = num_prototypes
+        self._net = feature_net
+        self._add_on = add_on_layers
+        self._classification = classification_layer
+        self._intermediate = intermediate_layer
+        assert backward_clamp_strategy in ["Identity", "Gated"]
+        print(f"Using backward clamp strategy: {backward_clamp_strategy}", flush=True)
+        self._is_clamp_backward_identity = backward_clamp_strategy == "Identity"
+        self._max_count = max_count
+        self._use_ste = use_ste
+        self._multiplier = classification_layer.normalization_multiplier
+        self.ste_round = STE_Round.apply
+        self.ste_clamp = ClampSTE.apply
+
+    def forward(self, xs, inference=False):
+        if use_hip(self):
+            return self._forward_hip(xs, inference)
+        features = self._net(xs)
+        proto_features = self._add_on(features)
+        counts = proto_features.sum(dim=(2, 3))
+        if self._use_ste:
+            clamped = self.ste_clamp(self.ste_round(counts), 0, self._max_count, self._is_clamp_backward_identity)
+        else:
+            clamped = torch.clamp(counts.round() if inference else counts, 0, self._max_count)
+        out = self._classification(self._intermediate(clamped))
+        return (proto_features, clamped, out) if inference else (proto_features, counts, out)
+
+    # -- HIP inference path ---------------------------------------------------------------
+    def _forward_hip(self, xs, inference):
+        K.require_device(xs, "input images")
+        feats = as_nhwc(self._net(xs))
+        act = list(self._add_on)[-1] if isinstance(self._add_on, nn.Sequential) else self._add_on
+        do_round = bool(self._use_ste or inference)
+        if isinstance(act, GumbelSoftmax):
+            logits = add_on_logits_hip(self._add_on, feats, activation=GumbelSoftmax)
+            noise = act.exp_noise
+            if noise is not None:
+                noise = noise.to(device=logits.device, dtype=torch.float32).contiguous()
+            seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())   # fresh noise per call
+            proto, hist = K.count_gumbel(logits, act.tau, noise, seed)
+            counts, clamped = K.count_finish(hist, None, self._max_count, do_round)
+        else:
+            logits = add_on_logits_hip(self._add_on, feats, activation=nn.Softmax)
+            proto, sums = K.softmax_pool(logits, pool_mode=1)
+            counts, clamped = K.count_finish(None, sums, self._max_count, do_round)
+        inter = intermediate_hip(self._intermediate, clamped)
+        cls = self._classification
+        _, out = K.nonneg_linear(inter, cls.weight, cls.bias, None)
+        return nhwc_as_nchw(proto), (clamped if inference else counts), out
+
+    def _calculate_counts_for_testing(self, proto_features):
+        return proto_features.sum(dim=(2, 3))
+
+    def get_prototype_importance_per_class(self, prototype_idx, classifier_input_scalars=None):
+        """count_pipnet.py:126-147."""
+        w_in = self._intermediate.prototype_to_classifier_input_weights(prototype_idx)
+        if classifier_input_scalars is not None:
+            assert classifier_input_scalars.shape == w_in.shape, \
+                f"Classifier input scalars must have the same shape as the classifier input weights " \
+                f"{tuple(w_in.shape)} vs {tuple(classifier_input_scalars.shape)}"
+            w_in = w_in * classifier_input_scalars
+        return torch.einsum("d,kd->k", torch.abs(w_in).to(self._classification.weight.device),
+                            self._classification.weight)
+
+    def get_prototype_importance(self, prototype_idx):
+        return self.get_prototype_importance_per_class(prototype_idx).sum().item()
+
+    def update_temperature(self, new_temperature):
+        for module in self._add_on.modules():
+            if isinstance(module, GumbelSoftmax):
+                module.tau = new_temperature
+                break
+
+
+def intermediate_hip(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """HIP forward of the count -> classifier-input layers (count_pipnet.py:393-417)."""
+    if isinstance(layer, IdentityIntermediate):
+        return x
+    if isinstance(layer, OneHotEncoder):
+        return K.count_encode(x, layer.num_bins, kind=0, do_round=layer.use_ste)
+    if isinstance(layer, LinearIntermediate):
+        w = layer.linear.weight[:, 0].contiguous()
+        return K.count_encode(x, layer.expansion_factor, kind=1, do_round=False, w=w)
+    if isinstance(layer, LinearFull):
+        return K.linear(x, layer.linear.weight)
+    if isinstance(layer, BilinearIntermediate):
+        e = K.linear(x, layer.embed.weight)
+        we = K.linear(e, layer.W.weight)
+        return K.linear(e, layer.V.weight, epilogue=_lib.EPI_MUL, r=we)
+    raise RuntimeError(f"CountPIPNet HIP path: unsupported intermediate layer {type(layer).__name__}")
+
+
+base_architecture_to_features = {
+    "convnext_tiny_26": convnext_tiny_26_features,
+    "convnext_tiny_13": convnext_tiny_13_features,
+}
+
+
+class NonNegLinear(nn.Module):
+    """count_pipnet.py:176-224 (Kaiming-uniform init, unlike pipnet.py's uninitialised one)."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, device=None, dtype=None) -> None:
+        super().__init__()
+        kw = {"device": device, "dtype": dtype}
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.empty((out_features, in_features), **kw))
+        self.normalization_multiplier = nn.Parameter(torch.ones((1,), requires_grad=True))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_features, **kw))
+        else:
+            self.register_parameter("bias", None)
+        self.reset_parameters()
+
+    def reset_parameters(self) -> None:
+        nn.init.kaiming_uniform_(self.weight, a=math.sqrt(5))
+        if self.bias is not None:
+            bound = 1 / math.sqrt(self.weight.shape[1]) if self.weight.shape[1] > 0 else 0
+            nn.init.uniform_(self.bias, -bound, bound)
+
+    def forward(self, input: torch.Tensor) -> torch.Tensor:
+        return F.linear(input, torch.relu(self.weight), self.bias)
+
+
+def detect_output_channels(features: nn.Module) -> int:
+    """count_pipnet.py:438-464: out_channels of the last Conv2d of the last features stage."""
+    if hasattr(features, "features") and len(features.features) > 0:
+        last_conv = None
+        for m in features.features[-1].modules():
+            if isinstance(m, nn.Conv2d):
+                last_conv = m
+        if last_conv is not None:
+            print(f"Detected {last_conv.out_channels} output channels from last conv layer", flush=True)
+            return last_conv.out_channels
+    raise RuntimeError("Could not detect output channels from the feature extractor.")
+
+
+def get_count_network(num_classes: int, args: argparse.Namespace, max_count: int = 3, use_ste: bool = True,
+                      device=None):
+    """count_pipnet.py:324-436 -> (CountPIPNet, num_prototypes)."""
+    if args.net not in base_architecture_to_features:
+        raise ValueError(f"Network '{args.net}' is not supported. "
+                         f"Supported networks: {list(base_architecture_to_features)}")
+    features = base_architecture_to_features[args.net](
+        pretrained=not args.disable_pretrained,
+        use_mid_layers=getattr(args, "use_mid_layers", False),
+        num_stages=getattr(args, "num_stages", 2))
+    in_ch = detect_output_channels(features)
+    activation = getattr(args, "activation", "gumbel_softmax")
+    act = nn.Softmax(dim=1) if activation == "softmax" else GumbelSoftmax(dim=1, tau=1.0)
+    if args.num_features == 0:
+        num_prototypes = in_ch
+        print(f"Number of prototypes: {num_prototypes}", flush=True)
+        add_on = nn.Sequential(act)
+    else:
+        num_prototypes = args.num_features
+        print(f"Number of prototypes set from {in_ch} to {num_prototypes}. Extra 1x1 conv layer added.", flush=True)
+        add_on = nn.Sequential(nn.Conv2d(in_ch, num_prototypes, kernel_size=1, stride=1, padding=0, bias=True), act)
+    kind = getattr(args, "intermediate_layer", "onehot")
+    positive_grad_strategy = getattr(args, "positive_grad_strategy", None)
+    print(f"Using positive gradient strategy: {positive_grad_strategy}", flush=True)
+    backward_clamp_strategy = getattr(args, "backward_clamp_strategy", "Gated")
+    if kind == "linear":
+        inter, dim = LinearIntermediate(num_prototypes, max_count), num_prototypes * max_count
+    elif kind == "linear_full":
+        inter, dim = LinearFull(num_prototypes, max_count), num_prototypes * max_count
+    elif kind == "bilinear":
+        inter, dim = BilinearIntermediate(num_prototypes, max_count), num_prototypes * max_count
+    elif kind == "onehot":
+        inter = OneHotEncoder(max_count, use_ste=use_ste, respect_active_grad=False, num_prototypes=num_prototypes,
+                              device=device, positive_grad_strategy=positive_grad_strategy)
+        dim = num_prototypes * max_count
+    elif kind == "identity":
+        inter, dim = IdentityIntermediate(num_prototypes, device=device), num_prototypes
+    else:
+        raise ValueError(f"Unknown intermediate layer type: {kind}")
+    classification = NonNegLinear(dim, num_classes, bias=getattr(args, "bias", False))
+    model = CountPIPNet(num_classes=num_classes, num_prototypes=num_prototypes, feature_net=features, args=args,
+                        add_on_layers=add_on, classification_layer=classification, intermediate_layer=inter,
+                        max_count=max_count, use_ste=use_ste, backward_clamp_strategy=backward_clamp_strategy)
+    return model, num_prototypes

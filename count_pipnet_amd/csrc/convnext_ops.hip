@@ -1,0 +1,256 @@
+// ConvNeXt-tiny non-GEMM stages on gfx950, NHWC fp32 (HBM/VALU-bound, no MFMA shape):
+//   * stem      Conv2d(3,96,k4,s4)+LayerNorm2d  -- reads the NCHW input directly
+//   * dwconv7   depthwise 7x7 (+bias) fused with the CNBlock LayerNorm
+//   * layernorm LayerNorm2d in front of each downsample conv
+// torchvision semantics restated in SURVEY.md 2.3; the reference builds the net in
+// features/convnext_features.py:38-94.
+#include "common.hpp"
+
+namespace {
+
+constexpr float LN_EPS = 1e-6f;
+
+// ---------------------------------------------------------------------------------------
+// stem: one workgroup per (image, output row); thread = (pixel, 24-channel group).
+// ---------------------------------------------------------------------------------------
+constexpr int STEM_C = 96, STEM_K = 48, STEM_WLD = 49;
+
+__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W,
+                                                   const float* __restrict__ w, const float* __restrict__ bias,
+                                                   const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                   float* __restrict__ y) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* wsm = sm;                                 // [96][49]
+  float* xin = sm + STEM_C * STEM_WLD;             // [3][4][W]
+  const int OH = H / 4, OW = W / 4;
+  const int b = blockIdx.x / OH, oy = blockIdx.x - (blockIdx.x / OH) * OH;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < STEM_C * STEM_K; i += 256) wsm[(i / STEM_K) * STEM_WLD + i % STEM_K] = w[i];
+  for (int i = tid; i < 12 * W; i += 256) {
+    const int c = i / (4 * W), r = i - c * 4 * W, ky = r / W, xx = r - ky * W;
+    xin[i] = x[(((int64_t)b * 3 + c) * H + 4 * oy + ky) * W + xx];
+  }
+  __syncthreads();
+  const int cg = tid & 3;
+  for (int px = tid >> 2; px < OW; px += 64) {
+    float in[STEM_K];
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int ky = 0; ky < 4; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 4; ++kx) in[c * 16 + ky * 4 + kx] = xin[(c * 4 + ky) * W + 4 * px + kx];
+    float o[24];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const int co = cg * 24 + j;
+      float a = bias[co];
+#pragma unroll
+      for (int k = 0; k < STEM_K; ++k) a = fmaf(wsm[co * STEM_WLD + k], in[k], a);
+      o[j] = a;
+      s += a;
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    const float mean = s * (1.0f / STEM_C);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < 24; ++j) {
+      const float d = o[j] - mean;
+      q = fmaf(d, d, q);
+    }
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    const float rstd = 1.0f / sqrtf(q * (1.0f / STEM_C) + LN_EPS);
+    float* dst = y + (((int64_t)b * OH + oy) * OW + px) * STEM_C + cg * 24;
+#pragma unroll
+    for (int j = 0; j < 24; j += 4) {
+      f32x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = cg * 24 + j + e;
+        v[e] = (o[j + e] - mean) * rstd * lnw[co] + lnb[co];
+      }
+      st4(dst + j, v);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// depthwise 7x7 + LayerNorm(C).  192 threads = G groups x (C/4) channel quads; group g
+// computes TX consecutive pixels of one output row with a sliding 7-column window held
+// in registers, then the row tile goes through LDS for the per-pixel LayerNorm (one
+// wave per pixel, two-pass mean / variance).
+// ---------------------------------------------------------------------------------------
+constexpr int DW_THREADS = 192;
+
+template <int C, int TX>
+__global__ __launch_bounds__(DW_THREADS) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
+                                                                const float* __restrict__ wp,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ lnw,
+                                                                const float* __restrict__ lnb,
+                                                                float* __restrict__ y) {
+  constexpr int QC = C / 4;
+  constexpr int G = DW_THREADS / QC;
+  constexpr int NP = G * TX;
+  constexpr int NJ = (C + 63) / 64;
+  __shared__ __attribute__((aligned(16))) float tile[NP * C];
+
+  const int tid = threadIdx.x;
+  const int q = tid % QC, g = tid / QC;
+  const int b = blockIdx.z, oy = blockIdx.y;
+  const int xblk = blockIdx.x * NP;
+  const int px0 = xblk + g * TX;
+
+  const f32x4 bq = ld4(bias + 4 * q);
+  f32x4 acc[TX];
+#pragma unroll
+  for (int i = 0; i < TX; ++i) acc[i] = bq;
+
+  for (int ky = 0; ky < 7; ++ky) {
+    const int iy = oy + ky - 3;
+    if (iy < 0 || iy >= H) continue;
+    const float* row = x + (((int64_t)b * H + iy) * W) * C + 4 * q;
+    f32x4 wk[7];
+#pragma unroll
+    for (int kx = 0; kx < 7; ++kx) wk[kx] = ld4(wp + (ky * 7 + kx) * C + 4 * q);
+#pragma unroll
+    for (int r = 0; r < TX + 6; ++r) {
+      const int ix = px0 + r - 3;
+      const f32x4 v = (ix >= 0 && ix < W) ? ld4(row + (int64_t)ix * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) {
+        const int px = r - kx;
+        if (px >= 0 && px < TX) acc[px] += v * wk[kx];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TX; ++i) st4(tile + (g * TX + i) * C + 4 * q, acc[i]);
+  __syncthreads();
+
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int pix = wv; pix < NP; pix += DW_THREADS / 64) {
+    const int ox = xblk + pix;
+    if (ox >= W) break;
+    float v[NJ];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      v[j] = (c < C) ? tile[pix * C + c] : 0.f;
+      s += v[j];
+    }
+    const float mean = wave_sum(s) * (1.0f / C);
+    float qq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      const float d = (c < C) ? v[j] - mean : 0.f;
+      qq = fmaf(d, d, qq);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
+    float* dst = y + (((int64_t)b * H + oy) * W + ox) * C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) dst[c] = (v[j] - mean) * rstd * lnw[c] + lnb[c];
+    }
+  }
+}
+
+template <int C, int TX>
+int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
+              const float* lnb, float* y, hipStream_t s) {
+  constexpr int NP = (DW_THREADS / (C / 4)) * TX;
+  const dim3 grid((W + NP - 1) / NP, H, B);
+  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw, lnb, y);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// row LayerNorm: one wave per row of C channels.
+// ---------------------------------------------------------------------------------------
+template <int NJ>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int C,
+                                                        const float* __restrict__ w, const float* __restrict__ b,
+                                                        float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* src = x + row * C;
+  float v[NJ];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < C ? src[c] : 0.f;
+    s += v[j];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    const float d = c < C ? v[j] - mean : 0.f;
+    q = fmaf(d, d, q);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + LN_EPS);
+  float* dst = y + row * C;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < C) dst[c] = (v[j] - mean) * rstd * w[c] + b[c];
+  }
+}
+
+}  // namespace
+
+extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, const float* w, const float* b,
+                                        const float* ln_w, const float* ln_b, float* y, void* stream) {
+  if (B < 0 || H < 4 || W < 4 || (H & 3) || (W & 3) || W > 4096) return PIPNET_ERR_ARG;
+  if (!x || !w || !b || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(y)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  const size_t shmem = (STEM_C * STEM_WLD + 12 * W) * sizeof(float);
+  hipLaunchKernelGGL(stem_kernel, dim3(B * (H / 4)), dim3(256), shmem, (hipStream_t)stream, x, H, W, w, b, ln_w,
+                     ln_b, y);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C, const float* w_packed,
+                                     const float* bias, const float* ln_w, const float* ln_b, float* y,
+                                     void* stream) {
+  if (B < 0 || H <= 0 || W <= 0) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !bias || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (C) {
+    case 96: return launch_dw<96, 7>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 192: return launch_dw<192, 7>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 384: return launch_dw<384, 14>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 768: return launch_dw<768, 13>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    default: return PIPNET_ERR_ARG;
+  }
+}
+
+extern "C" int pipnet_layernorm_f32(const float* x, int64_t rows, int C, const float* w, const float* b, float* y,
+                                    void* stream) {
+  if (rows < 0 || C <= 0 || C > 2048 || !x || !w || !b || !y) return PIPNET_ERR_ARG;
+  if (rows == 0) return PIPNET_OK;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  const int nj = (C + 63) / 64;
+  if (nj <= 2) hipLaunchKernelGGL(layernorm_kernel<2>, grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 3) hipLaunchKernelGGL(layernorm_kernel<3>, grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 6) hipLaunchKernelGGL(layernorm_kernel<6>, grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 12) hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else hipLaunchKernelGGL(layernorm_kernel<32>, grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}

@@ -1,0 +1,321 @@
+// Prototype heads on gfx950 (HBM-bound wavefront-reduction kernels):
+//   * softmax_pool   nn.Softmax(dim=1) over P channels per patch + AdaptiveMaxPool2d(1)
+//                    (or spatial sum), proto map written exactly once      -- pipnet.py:33-34
+//   * nonneg_linear  where(x<0.1,0,x) then F.linear(x, relu(W), b)         -- pipnet.py:36-37,70-71
+//   * count_gumbel   F.gumbel_softmax(hard=True) + per-prototype count      -- count_pipnet.py:83-88
+//   * count_finish   STE_Round / ClampSTE forwards                          -- count_pipnet.py:90-97
+//   * count_encode   OneHotEncoder / LinearIntermediate forwards            -- count_pipnet_utils.py
+// One wave owns one patch: lane l holds channels l, l+64, ... so every HBM access is a
+// coalesced 256-B row segment, and the per-patch reductions are 64-lane butterflies.
+#include "common.hpp"
+
+namespace {
+
+constexpr int HEAD_THREADS = 256;
+constexpr int PIX_PER_BLOCK = 32;
+
+// ---------------------------------------------------------------------------------------
+template <int NJ, int MODE>   // MODE 0 = max pool, 1 = sum pool
+__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const float* __restrict__ feat, int HW, int P,
+                                                                    float* __restrict__ proto,
+                                                                    float* __restrict__ pooled) {
+  __shared__ float red[HEAD_THREADS / 64][NJ * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  float racc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) racc[j] = 0.f;   // softmax outputs are >= 0
+  for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
+    const int pix = pix0 + pi;
+    if (pix >= HW) break;
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+    float v[NJ];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      v[j] = c < P ? feat[base + c] : -INFINITY;
+      m = fmaxf(m, v[j]);
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      v[j] = c < P ? expf(v[j] - m) : 0.f;
+      s += v[j];
+    }
+    const float inv = 1.0f / wave_sum(s);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < P) {
+        const float yv = v[j] * inv;
+        proto[base + c] = yv;
+        racc[j] = MODE == 0 ? fmaxf(racc[j], yv) : racc[j] + yv;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) red[wv][lane + 64 * j] = racc[j];
+  __syncthreads();
+  for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
+    float r = red[0][c];
+#pragma unroll
+    for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
+    float* dst = pooled + (int64_t)b * P + c;
+    if (MODE == 0)   // non-negative floats order like their bit patterns
+      atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
+    else
+      atomicAdd(dst, r);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// NonNegLinear: one workgroup per image, x' staged in LDS, one wave per output class.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float* __restrict__ x, int D,
+                                                                     const float* __restrict__ W,
+                                                                     const float* __restrict__ bias, int K,
+                                                                     int apply_thresh, float thresh,
+                                                                     float* __restrict__ x_out,
+                                                                     float* __restrict__ out) {
+  extern __shared__ float xs[];
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
+    float v = x[(int64_t)b * D + c];
+    if (apply_thresh && v < thresh) v = 0.f;
+    xs[c] = v;
+    if (x_out) x_out[(int64_t)b * D + c] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = wv; k < K; k += HEAD_THREADS / 64) {
+    const float* wr = W + (int64_t)k * D;
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s = fmaf(xs[c], fmaxf(wr[c], 0.f), s);
+    s = wave_sum(s);
+    if (lane == 0) out[(int64_t)b * K + k] = s + (bias ? bias[k] : 0.f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11) -> one Exp(1) draw per element index.
+// ---------------------------------------------------------------------------------------
+PIPNET_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
+  const uint64_t p = (uint64_t)a * b;
+  hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+
+PIPNET_DEV float philox_exp(uint64_t seed, uint64_t ctr) {
+  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0u, c3 = 0u;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    const uint32_t lo0 = mulhilo(0xD2511F53u, c0, hi0);
+    const uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, hi1);
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  const float u = ((float)(c0 >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  return -logf(u);
+}
+
+template <int NJ>
+__global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float* __restrict__ logits, int HW, int P,
+                                                                    float inv_tau,
+                                                                    const float* __restrict__ exp_noise,
+                                                                    uint64_t seed, uint64_t offset,
+                                                                    float* __restrict__ proto,
+                                                                    int32_t* __restrict__ hist) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
+    const int pix = pix0 + pi;
+    if (pix >= HW) break;
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+    float z[NJ];
+    float m = -INFINITY;
+    int mi = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < P) {
+        const int64_t e_idx = ((int64_t)b * P + c) * HW + pix;      // NCHW element index
+        const float E = exp_noise ? exp_noise[e_idx] : philox_exp(seed, offset + (uint64_t)e_idx);
+        z[j] = (logits[base + c] - logf(E)) * inv_tau;
+        if (z[j] > m) { m = z[j]; mi = c; }
+      } else {
+        z[j] = -INFINITY;
+      }
+    }
+    // wave argmax, first index on ties
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float om = __shfl_xor(m, o, 64);
+      const int oi = __shfl_xor(mi, o, 64);
+      if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) s += (lane + 64 * j < P) ? expf(z[j] - m) : 0.f;
+    const float ysoft = 1.0f / wave_sum(s);              // softmax value at the argmax
+    const float hard = (1.0f - ysoft) + ysoft;           // y_hard - y_soft + y_soft
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < P) proto[base + c] = (c == mi) ? hard : 0.f;
+    }
+    if (lane == 0) atomicAdd(hist + (int64_t)b * P + mi, 1);
+  }
+}
+
+__global__ void count_finish_kernel(const int32_t* __restrict__ hist, const float* __restrict__ sums, int64_t n,
+                                    float max_count, int do_round, float* __restrict__ raw,
+                                    float* __restrict__ clamped) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float c = hist ? (float)hist[i] : sums[i];
+    if (raw) raw[i] = c;
+    const float r = do_round ? rintf(c) : c;   // torch.round: half to even
+    clamped[i] = fminf(fmaxf(r, 0.f), max_count);
+  }
+}
+
+__global__ void count_encode_kernel(const float* __restrict__ x, int64_t BP, int C, int kind, int do_round,
+                                    const float* __restrict__ w, float* __restrict__ out) {
+  const int64_t n = BP * C;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bp = i / C;
+    const int c = (int)(i - bp * C);
+    float v = x[bp];
+    if (kind == 0) {
+      if (do_round) v = rintf(v);
+      int idx = (int)v - 1;                    // .long() truncates toward zero
+      idx = idx < 0 ? 0 : (idx > C - 1 ? C - 1 : idx);
+      out[i] = (v > 0.1f && c == idx) ? 1.0f : 0.0f;
+    } else {
+      out[i] = v * w[c];
+    }
+  }
+}
+
+int nj_bucket(int P) {
+  const int nj = (P + 63) / 64;
+  if (nj <= 1) return 1;
+  if (nj <= 2) return 2;
+  if (nj <= 4) return 4;
+  if (nj <= 8) return 8;
+  if (nj <= 12) return 12;
+  if (nj <= 16) return 16;
+  if (nj <= 32) return 32;
+  return -1;
+}
+
+}  // namespace
+
+#define PIPNET_NJ_SWITCH(NJV, CALL) \
+  switch (NJV) {                    \
+    case 1: CALL(1); break;         \
+    case 2: CALL(2); break;         \
+    case 4: CALL(4); break;         \
+    case 8: CALL(8); break;         \
+    case 12: CALL(12); break;       \
+    case 16: CALL(16); break;       \
+    case 32: CALL(32); break;       \
+    default: return PIPNET_ERR_ARG; \
+  }
+
+extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
+                                       float* pooled, void* stream) {
+  if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1)) return PIPNET_ERR_ARG;
+  if (!feat || !proto || !pooled) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  const int nj = nj_bucket(P);
+  if (nj < 0) return PIPNET_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(pooled, 0, sizeof(float) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+#define SP_CALL(N)                                                                                       \
+  if (pool_mode == 0)                                                                                    \
+    hipLaunchKernelGGL((softmax_pool_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled); \
+  else                                                                                                   \
+    hipLaunchKernelGGL((softmax_pool_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled);
+  PIPNET_NJ_SWITCH(nj, SP_CALL)
+#undef SP_CALL
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,
+                                        int apply_thresh, float thresh, float* x_out, float* out, void* stream) {
+  if (B < 0 || D <= 0 || K <= 0 || D > 16384 || !x || !W || !out) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(nonneg_linear_kernel, dim3(B), dim3(HEAD_THREADS), sizeof(float) * D, (hipStream_t)stream, x,
+                     D, W, bias, K, apply_thresh, thresh, x_out, out);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau, const float* exp_noise,
+                                       uint64_t seed, uint64_t offset, float* proto, int32_t* hist, void* stream) {
+  if (B < 0 || HW <= 0 || P <= 0 || !(tau > 0.f) || !logits || !proto || !hist) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  const int nj = nj_bucket(P);
+  if (nj < 0) return PIPNET_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const float inv_tau = 1.0f / tau;
+#define CG_CALL(N)                                                                                              \
+  hipLaunchKernelGGL((count_gumbel_kernel<N>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, exp_noise, \
+                     seed, offset, proto, hist);
+  PIPNET_NJ_SWITCH(nj, CG_CALL)
+#undef CG_CALL
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_count_finish_f32(const int32_t* hist, const float* sums, int B, int P, int max_count,
+                                       int do_round, float* counts_raw, float* clamped, void* stream) {
+  if (B < 0 || P <= 0 || max_count < 0 || (!hist && !sums) || !clamped) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  const int64_t n = (int64_t)B * P;
+  const int blocks = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(count_finish_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, hist, sums, n,
+                     (float)max_count, do_round, counts_raw, clamped);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_count_encode_f32(const float* x, int B, int P, int C, int kind, int do_round, const float* w,
+                                       float* out, void* stream) {
+  if (B < 0 || P <= 0 || C <= 0 || (kind != 0 && kind != 1) || !x || !out || (kind == 1 && !w)) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  const int64_t n = (int64_t)B * P * C;
+  const int blocks = (int)((n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048);
+  hipLaunchKernelGGL(count_encode_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, (int64_t)B * P, C,
+                     kind, do_round, w, out);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_amd_abi_version(void) { return 1; }
+
+extern "C" const char* pipnet_amd_status_string(int status) {
+  switch (status) {
+    case PIPNET_OK: return "ok";
+    case PIPNET_ERR_ARG: return "invalid argument (shape/size/configuration)";
+    case PIPNET_ERR_ALIGN: return "pointer or leading dimension not 16-byte aligned";
+    case PIPNET_ERR_LAUNCH: return "kernel launch failed";
+    case PIPNET_ERR_HIP: return "HIP runtime error";
+    default: return "unknown status";
+  }
+}

@@ -1,0 +1,178 @@
+"""Tensor-level wrappers over the C-ABI (one function per HIP entry point).
+
+Every wrapper validates device / dtype / contiguity, allocates its outputs on the input's
+device and enqueues on torch's *current* HIP stream, so the calls compose with torch
+streams, events and graph capture.  Nothing here computes on the host.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+Tensor = torch.Tensor
+
+
+# Optional instrumentation: hook(kernel_name, algorithmic_flops, launch_fn) wraps every MFMA
+# GEMM launch (bench.py brackets them with HIP events on the launching stream).
+_launch_hook = None
+
+
+def set_launch_hook(hook) -> None:
+    global _launch_hook
+    _launch_hook = hook
+
+
+def _launch(kname: str, flops: float, fn) -> None:
+    if _launch_hook is None:
+        fn()
+    else:
+        _launch_hook(kname, flops, fn)
+
+
+def _ptr(t: Optional[Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_device(t: Tensor, what: str = "input") -> None:
+    if not (t.is_cuda and t.dtype == torch.float32):
+        raise RuntimeError(
+            f"count_pipnet_amd: the HIP inference path needs a float32 ROCm device tensor for {what} "
+            f"(got device={t.device}, dtype={t.dtype}); there is no CPU fallback. Move the model and "
+            "inputs to a GPU, or run the autograd path (train mode / grad enabled).")
+
+
+def _chk(t: Tensor, what: str, contiguous: bool = True) -> None:
+    require_device(t, what)
+    if contiguous and not t.is_contiguous():
+        raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
+
+
+def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = _lib.EPI_NONE,
+           scale: Optional[Tensor] = None, r: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Tensor:
+    """out[M,N] = epi(a[M,K] @ w[N,K]^T).  a may be any 2-D row-major view with unit col stride."""
+    require_device(a, "linear input")
+    _chk(w, "weight")
+    if a.dim() != 2 or w.dim() != 2 or a.stride(1) != 1:
+        raise RuntimeError("linear: expects 2-D operands with unit column stride")
+    m, k = a.shape
+    n = w.shape[0]
+    if w.shape[1] != k:
+        raise RuntimeError(f"linear: K mismatch {tuple(a.shape)} x {tuple(w.shape)}")
+    if out is None:
+        out = torch.empty((m, n), device=a.device, dtype=torch.float32)
+    ldr = r.stride(0) if r is not None else 0
+    _launch(f"gemm_f32_tn_kernel<{epilogue}, 0>", 2.0 * m * n * k,
+            lambda: _lib.call("pipnet_linear_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias), _ptr(scale),
+                              _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue, _stream(a)))
+    return out
+
+
+def conv2x2(x_nhwc: Tensor, w_packed: Tensor, bias: Optional[Tensor], stride: int) -> Tensor:
+    _chk(x_nhwc, "conv2x2 input")
+    b, h, w, cin = x_nhwc.shape
+    cout = w_packed.shape[0]
+    oh, ow = (h - 2) // stride + 1, (w - 2) // stride + 1
+    y = torch.empty((b, oh, ow, cout), device=x_nhwc.device, dtype=torch.float32)
+    epi = _lib.EPI_BIAS if bias is not None else _lib.EPI_NONE
+    _launch(f"gemm_f32_tn_kernel<{epi}, 1>", 2.0 * b * oh * ow * cout * 4 * cin,
+            lambda: _lib.call("pipnet_conv2x2_f32", x_nhwc.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
+                              cout, stride, y.data_ptr(), _stream(x_nhwc)))
+    return y
+
+
+def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tensor) -> Tensor:
+    _chk(x_nchw, "network input (NCHW)")
+    n, c, h, wd = x_nchw.shape
+    if c != 3:
+        raise RuntimeError(f"convnext stem expects 3 input channels, got {c}")
+    y = torch.empty((n, h // 4, wd // 4, 96), device=x_nchw.device, dtype=torch.float32)
+    _lib.call("pipnet_convnext_stem_f32", x_nchw.data_ptr(), n, h, wd, w.data_ptr(), b.data_ptr(), ln_w.data_ptr(),
+              ln_b.data_ptr(), y.data_ptr(), _stream(x_nchw))
+    return y
+
+
+def dwconv7_ln(x_nhwc: Tensor, w_packed: Tensor, bias: Tensor, ln_w: Tensor, ln_b: Tensor,
+               out: Optional[Tensor] = None) -> Tensor:
+    _chk(x_nhwc, "dwconv input")
+    b, h, w, c = x_nhwc.shape
+    y = torch.empty_like(x_nhwc) if out is None else out
+    _lib.call("pipnet_dwconv7_ln_f32", x_nhwc.data_ptr(), b, h, w, c, w_packed.data_ptr(), bias.data_ptr(),
+              ln_w.data_ptr(), ln_b.data_ptr(), y.data_ptr(), _stream(x_nhwc))
+    return y
+
+
+def layernorm(x: Tensor, w: Tensor, b: Tensor, out: Optional[Tensor] = None) -> Tensor:
+    _chk(x, "layernorm input")
+    c = x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    _lib.call("pipnet_layernorm_f32", x.data_ptr(), x.numel() // c, c, w.data_ptr(), b.data_ptr(), y.data_ptr(),
+              _stream(x))
+    return y
+
+
+def softmax_pool(feat_nhwc: Tensor, pool_mode: int) -> Tuple[Tensor, Tensor]:
+    """feat [B,h,w,P] -> (proto [B,h,w,P], pooled [B,P]); pool 0 = max, 1 = sum."""
+    _chk(feat_nhwc, "prototype logits")
+    b, h, w, p = feat_nhwc.shape
+    proto = torch.empty_like(feat_nhwc)
+    pooled = torch.empty((b, p), device=feat_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_softmax_pool_f32", feat_nhwc.data_ptr(), b, h * w, p, pool_mode, proto.data_ptr(),
+              pooled.data_ptr(), _stream(feat_nhwc))
+    return proto, pooled
+
+
+def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float]) -> Tuple[Tensor, Tensor]:
+    """(x', out) with x' = where(x < thresh, 0, x) (or x) and out = x' relu(w)^T + bias."""
+    _chk(x, "classifier input")
+    _chk(w, "classifier weight")
+    b, d = x.shape
+    k = w.shape[0]
+    x_out = torch.empty_like(x)
+    out = torch.empty((b, k), device=x.device, dtype=torch.float32)
+    _lib.call("pipnet_nonneg_linear_f32", x.data_ptr(), b, d, w.data_ptr(), _ptr(bias), k,
+              0 if thresh is None else 1, 0.0 if thresh is None else float(thresh), x_out.data_ptr(),
+              out.data_ptr(), _stream(x))
+    return x_out, out
+
+
+def count_gumbel(logits_nhwc: Tensor, tau: float, exp_noise_nchw: Optional[Tensor], seed: int,
+                 offset: int = 0) -> Tuple[Tensor, Tensor]:
+    """Hard Gumbel-softmax one-hot map [B,h,w,P] + int32 histogram [B,P]."""
+    _chk(logits_nhwc, "prototype logits")
+    b, h, w, p = logits_nhwc.shape
+    if exp_noise_nchw is not None:
+        _chk(exp_noise_nchw, "exp noise")
+        if tuple(exp_noise_nchw.shape) != (b, p, h, w):
+            raise RuntimeError(f"exp noise shape {tuple(exp_noise_nchw.shape)} != {(b, p, h, w)}")
+    proto = torch.empty_like(logits_nhwc)
+    hist = torch.empty((b, p), device=logits_nhwc.device, dtype=torch.int32)
+    _lib.call("pipnet_count_gumbel_f32", logits_nhwc.data_ptr(), b, h * w, p, float(tau), _ptr(exp_noise_nchw),
+              int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), proto.data_ptr(), hist.data_ptr(),
+              _stream(logits_nhwc))
+    return proto, hist
+
+
+def count_finish(hist: Optional[Tensor], sums: Optional[Tensor], max_count: int, do_round: bool) -> Tuple[Tensor, Tensor]:
+    ref = hist if hist is not None else sums
+    b, p = ref.shape
+    raw = torch.empty((b, p), device=ref.device, dtype=torch.float32)
+    clamped = torch.empty_like(raw)
+    _lib.call("pipnet_count_finish_f32", _ptr(hist), _ptr(sums), b, p, int(max_count), int(do_round),
+              raw.data_ptr(), clamped.data_ptr(), _stream(ref))
+    return raw, clamped
+
+
+def count_encode(x: Tensor, c: int, kind: int, do_round: bool, w: Optional[Tensor] = None) -> Tensor:
+    _chk(x, "counts")
+    b, p = x.shape
+    out = torch.empty((b, p * c), device=x.device, dtype=torch.float32)
+    _lib.call("pipnet_count_encode_f32", x.data_ptr(), b, p, c, kind, int(do_round), _ptr(w), out.data_ptr(),
+              _stream(x))
+    return out

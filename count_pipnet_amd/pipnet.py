@@ -1,0 +1,154 @@
+"""PIP-Net -- drop-in for ``pipnet/pipnet.py`` (model, NonNegLinear, factories).
+
+``PIPNet.forward(xs, inference=False) -> (proto_features, pooled, out)`` keeps the
+reference signature, attribute names (``_net``, ``_add_on``, ``_pool``,
+``_classification``, ``_multiplier``, ``_num_*``) and ``state_dict`` keys.  In eval mode
+with grad disabled the whole forward runs on HIP kernels:
+
+  backbone (NHWC)  ->  [1x1 add-on on MFMA]  ->  fused per-patch softmax + spatial max-pool
+  (proto map written once, channels_last)  ->  fused threshold + NonNegLinear.
+
+``_classification.weight`` is read at call time (callers mutate it in place between
+batches, ``pipnet/test.py:71-73``).
+"""
+from __future__ import annotations
+
+import argparse
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch import Tensor
+
+from . import _lib
+from . import kernels as K
+from .backend import use_hip
+from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
+from .resnet_features import (resnet18_features, resnet34_features, resnet50_features, resnet50_features_inat,
+                              resnet101_features, resnet152_features)
+
+PRESENCE_THRESHOLD = 0.1   # pipnet.py:36
+
+
+class PIPNet(nn.Module):
+    def __init__(self, num_classes: int, num_prototypes: int, feature_net: nn.Module, args: argparse.Namespace,
+                 add_on_layers: nn.Module, pool_layer: nn.Module, classification_layer: nn.Module):
+        super().__init__()
+        assert num_classes > 0
+        self._num_features = args.num_features
+        self._num_classes = num_classes
+        self._num_prototypes = num_prototypes
+        self._net = feature_net
+        self._add_on = add_on_layers
+        self._pool = pool_layer
+        self._classification = classification_layer
+        self._multiplier = classification_layer.normalization_multiplier
+
+    def forward(self, xs: Tensor, inference: bool = False):
+        if use_hip(self):
+            return self._forward_hip(xs, inference)
+        features = self._net(xs)
+        proto_features = self._add_on(features)
+        pooled = self._pool(proto_features)
+        if inference:
+            clamped_pooled = torch.where(pooled < PRESENCE_THRESHOLD, 0.0, pooled)
+            return proto_features, clamped_pooled, self._classification(clamped_pooled)
+        return proto_features, pooled, self._classification(pooled)
+
+    # -- HIP inference path ---------------------------------------------------------------
+    def _forward_hip(self, xs: Tensor, inference: bool):
+        K.require_device(xs, "input images")
+        feats = as_nhwc(self._net(xs))                     # [B,h,w,C] NHWC
+        logits = add_on_logits_hip(self._add_on, feats)    # [B,h,w,P]
+        if not (isinstance(self._pool, nn.Sequential) and isinstance(self._pool[0], nn.AdaptiveMaxPool2d)):
+            raise RuntimeError("PIPNet HIP path expects _pool = Sequential(AdaptiveMaxPool2d(1), Flatten())")
+        proto, pooled = K.softmax_pool(logits, pool_mode=0)
+        cls = self._classification
+        clamped, out = K.nonneg_linear(pooled, cls.weight, cls.bias, PRESENCE_THRESHOLD if inference else None)
+        return nhwc_as_nchw(proto), (clamped if inference else pooled), out
+
+
+def add_on_logits_hip(add_on: nn.Module, feats: Tensor, activation=nn.Softmax) -> Tensor:
+    """Apply the (optional) 1x1 prototype projection of ``_add_on`` on MFMA; returns NHWC
+    logits.  The trailing activation module is applied by the caller's fused head kernel."""
+    mods = list(add_on) if isinstance(add_on, nn.Sequential) else [add_on]
+    if not mods or not isinstance(mods[-1], activation) or getattr(mods[-1], "dim", 1) != 1:
+        raise RuntimeError(f"HIP head expects _add_on to end with {activation.__name__}(dim=1), got {add_on}")
+    if len(mods) == 1:
+        return feats
+    conv = mods[0]
+    if not (len(mods) == 2 and isinstance(conv, nn.Conv2d) and conv.kernel_size == (1, 1)
+            and conv.stride == (1, 1) and conv.groups == 1):
+        raise RuntimeError(f"HIP head expects _add_on = [Conv2d 1x1, activation], got {add_on}")
+    b, h, w, c = feats.shape
+    p = conv.out_channels
+    y = K.linear(feats.view(-1, c), conv.weight.view(p, c), conv.bias,
+                 _lib.EPI_BIAS if conv.bias is not None else _lib.EPI_NONE)
+    return y.view(b, h, w, p)
+
+
+base_architecture_to_features = {
+    "resnet18": resnet18_features,
+    "resnet34": resnet34_features,
+    "resnet50": resnet50_features,
+    "resnet50_inat": resnet50_features_inat,
+    "resnet101": resnet101_features,
+    "resnet152": resnet152_features,
+    "convnext_tiny_26": convnext_tiny_26_features,
+    "convnext_tiny_13": convnext_tiny_13_features,
+}
+
+
+class NonNegLinear(nn.Module):
+    """pipnet.py:54-71: F.linear(x, relu(W), b); W uninitialised (torch.empty) like the reference."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, device=None, dtype=None) -> None:
+        super().__init__()
+        kw = {"device": device, "dtype": dtype}
+        self.in_features = in_features
+        self.out_features = out_features
+        self.weight = nn.Parameter(torch.empty((out_features, in_features), **kw))
+        self.normalization_multiplier = nn.Parameter(torch.ones((1,), requires_grad=True))
+        if bias:
+            self.bias = nn.Parameter(torch.empty(out_features, **kw))
+        else:
+            self.register_parameter("bias", None)
+
+    def forward(self, input: Tensor) -> Tensor:
+        return F.linear(input, torch.relu(self.weight), self.bias)
+
+
+def get_pip_network(num_classes: int, args: argparse.Namespace):
+    """pipnet.py:74-115."""
+    if "convnext" in args.net:
+        backbone = base_architecture_to_features[args.net](
+            pretrained=not args.disable_pretrained,
+            use_mid_layers=getattr(args, "use_mid_layers", False),
+            num_stages=getattr(args, "num_stages", 2))
+    elif "res" in args.net:
+        backbone = base_architecture_to_features[args.net](pretrained=not args.disable_pretrained)
+    else:
+        raise Exception("other base architecture NOT implemented")
+    in_ch = [m for m in backbone.modules() if isinstance(m, nn.Conv2d)][-1].out_channels
+    if args.num_features == 0:
+        num_prototypes = in_ch
+        print("Number of prototypes: ", num_prototypes, flush=True)
+        add_on = nn.Sequential(nn.Softmax(dim=1))
+    else:
+        num_prototypes = args.num_features
+        print("Number of prototypes set from", in_ch, "to", num_prototypes,
+              ". Extra 1x1 conv layer added. Not recommended.", flush=True)
+        add_on = nn.Sequential(
+            nn.Conv2d(in_channels=in_ch, out_channels=num_prototypes, kernel_size=1, stride=1, padding=0, bias=True),
+            nn.Softmax(dim=1))
+    pool = nn.Sequential(nn.AdaptiveMaxPool2d(output_size=(1, 1)), nn.Flatten())
+    classification = NonNegLinear(num_prototypes, num_classes, bias=bool(args.bias))
+    return backbone, add_on, pool, classification, num_prototypes
+
+
+def get_pipnet(num_classes: int, args: argparse.Namespace):
+    """pipnet.py:117-139 -> (PIPNet, num_prototypes)."""
+    feature_net, add_on, pool, classification, num_prototypes = get_pip_network(num_classes, args)
+    model = PIPNet(num_classes=num_classes, num_prototypes=num_prototypes, feature_net=feature_net, args=args,
+                   add_on_layers=add_on, pool_layer=pool, classification_layer=classification)
+    return model, num_prototypes

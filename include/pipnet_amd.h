@@ -1,0 +1,121 @@
+/*
+ * pipnet_amd.h -- C-ABI of the MI355X-native PIP-Net / CountPIPNet inference path.
+ *
+ * The reference (TarasKutsyk/Count_PIPNet) has no native code and no FFI: its boundary is
+ * the Python nn.Module contract of pipnet/pipnet.py and pipnet/count_pipnet.py
+ * (SURVEY.md 8b).  These entry points are what a ctypes / torch-extension binding of that
+ * forward binds: every op of the hot path's ATen sequence as one
+ * stream-ordered call.  Plain pointers and sizes only (no torch types).
+ *
+ * Conventions
+ *   - all tensors are float32 device pointers (HBM), activations NHWC ("channels_last"),
+ *     the network input NCHW exactly as the reference receives it;
+ *   - ``stream`` is a hipStream_t (NULL = default stream); calls only enqueue work;
+ *   - the return value is a PIPNET_* status; the Python host layer raises RuntimeError
+ *     on anything but PIPNET_OK (the reference raises Python exceptions).
+ *   - re-entrant: no global mutable state; callers own every buffer.
+ */
+#ifndef PIPNET_AMD_H
+#define PIPNET_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PIPNET_OK 0
+#define PIPNET_ERR_ARG 1        /* bad shape / size / unsupported configuration */
+#define PIPNET_ERR_ALIGN 2      /* pointer or leading dimension not 16-byte aligned */
+#define PIPNET_ERR_LAUNCH 3     /* hipLaunchKernel failed (hipGetLastError) */
+#define PIPNET_ERR_HIP 4        /* other HIP runtime error */
+
+/* GEMM epilogues for pipnet_linear_f32 */
+#define PIPNET_EPI_NONE 0       /* C = A W^T                                              */
+#define PIPNET_EPI_BIAS 1       /* C = A W^T + b                                          */
+#define PIPNET_EPI_BIAS_GELU 2  /* C = gelu_erf(A W^T + b)          (CNBlock Linear1+GELU) */
+#define PIPNET_EPI_RESID 3      /* C = R + s * (A W^T + b)   (CNBlock Linear2*layer_scale+x)*/
+#define PIPNET_EPI_MUL 4        /* C = (A W^T) * R          (BilinearIntermediate W(e)*V(e)) */
+
+int pipnet_amd_abi_version(void);
+const char* pipnet_amd_status_string(int status);
+
+/* Dense fp32 linear / 1x1 conv on MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
+ *   C[M,N] (ldc) = epi( A[M,K] (lda) * W[N,K]^T )
+ * Replaces F.linear / nn.Linear (torchvision CNBlock block.3 / block.5),
+ * the 1x1 add-on Conv2d (pipnet.py:99-104, count_pipnet.py:376-381) and the
+ * Bilinear/LinearFull intermediate Linears (count_pipnet_utils.py:342-385, :387-444).
+ * K % 4 == 0, lda/ldc/ldr % 4 == 0, pointers 16-B aligned.  bias/scale: [N] or NULL;
+ * R (resid / other): [M,N] with leading dimension ldr (may alias C for in-place residual). */
+int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
+                      const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
+                      int M, int N, int K, int epilogue, void* stream);
+
+/* ConvNeXt downsample conv, k=2, stride s in {1,2}, no padding, as implicit GEMM on MFMA.
+ * x: [B,H,W,Cin] NHWC (already LayerNorm2d-normalised), w_packed: [Cout][2][2][Cin]
+ * (torch weight [Cout,Cin,2,2] permuted), y: [B,OH,OW,Cout], OH=(H-2)/s+1.
+ * Replaces features.{2,4,6}.1 of torchvision ConvNeXt with the stride patch of
+ * features/convnext_features.py:5-15.  Cin % 32 == 0. */
+int pipnet_conv2x2_f32(const float* x, int B, int H, int W, int Cin, const float* w_packed,
+                       const float* bias, int Cout, int stride, float* y, void* stream);
+
+/* ConvNeXt stem: Conv2d(3,96,k4,s4,bias) + LayerNorm2d(96, eps 1e-6)  (features.0).
+ * x: [B,3,H,W] NCHW (the reference's own input layout), w: [96,3,4,4] as torch stores it,
+ * y: [B,H/4,W/4,96] NHWC. */
+int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, const float* w, const float* b,
+                             const float* ln_w, const float* ln_b, float* y, void* stream);
+
+/* CNBlock front half: depthwise Conv2d 7x7 pad 3 (+bias) + LayerNorm(C, eps 1e-6).
+ * x, y: [B,H,W,C] NHWC, w_packed: [49][C] (torch [C,1,7,7] transposed).
+ * C in {96,192,384,768}. */
+int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C, const float* w_packed,
+                          const float* bias, const float* ln_w, const float* ln_b, float* y,
+                          void* stream);
+
+/* Row LayerNorm over the last dim (LayerNorm2d on NHWC), eps 1e-6: y = LN(x) * w + b. */
+int pipnet_layernorm_f32(const float* x, int64_t rows, int C, const float* w, const float* b,
+                         float* y, void* stream);
+
+/* PIP-Net head, part 1 (pipnet.py:33-34): per-pixel softmax over P prototype channels
+ * (nn.Softmax(dim=1)), proto written once (NHWC), fused spatial pooling:
+ *   pool_mode 0 -> pooled[b,p] = max over pixels (AdaptiveMaxPool2d(1)+Flatten)
+ *   pool_mode 1 -> pooled[b,p] = sum over pixels (CountPIPNet softmax activation, :88)
+ * feat, proto: [B,HW,P]; pooled: [B,P] (zeroed by this call before accumulation). */
+int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
+                            float* pooled, void* stream);
+
+/* NonNegLinear (pipnet.py:54-71, count_pipnet.py:176-224): out = x' relu(W)^T + b with
+ * x' = where(x < thresh, 0, x) when apply_thresh (pipnet.py:36, inference) else x.
+ * x: [B,D], W: [K,D] read at call time (callers mutate it in place, test.py:73),
+ * bias [K] or NULL, x_out: [B,D] receives x' (may be NULL), out: [B,K]. */
+int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias,
+                             int K, int apply_thresh, float thresh, float* x_out, float* out,
+                             void* stream);
+
+/* CountPIPNet Gumbel-softmax (eval, hard=True) + spatial count (count_pipnet_utils.py:36-38,
+ * count_pipnet.py:88): per pixel z = (x - log E)/tau, one-hot at argmax written as the
+ * straight-through value (1 - y) + y, all other channels exactly 0, and hist[b,p] += 1.
+ * E ~ Exp(1) is read from exp_noise ([B,P,HW], the NCHW layout of torch's draw) when
+ * non-NULL, else generated in-kernel by Philox4x32-10 keyed by (seed, offset + element).
+ * logits, proto: [B,HW,P]; hist: [B,P] int32 (zeroed by this call). */
+int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau,
+                            const float* exp_noise, uint64_t seed, uint64_t offset, float* proto,
+                            int32_t* hist, void* stream);
+
+/* Count finish (count_pipnet.py:88-97): counts_raw = float(hist) (or sums when hist is
+ * NULL), clamped = clamp(round?(counts), 0, max_count) -- round when do_round.
+ * sums: [B,P] float (softmax activation path) used when hist == NULL. */
+int pipnet_count_finish_f32(const int32_t* hist, const float* sums, int B, int P, int max_count,
+                            int do_round, float* counts_raw, float* clamped, void* stream);
+
+/* Elementwise count encodings into [B, P*C] (p-major):
+ *   kind 0 (OneHotEncoder, count_pipnet_utils.py:141-185): one-hot at clamp(int(x)-1,0,C-1)
+ *          where x > 0.1, x rounded first when do_round (ModifiedSTEFunction :201-217);
+ *   kind 1 (LinearIntermediate, :471-539): out[b,p*C+c] = x[b,p] * w[c]. */
+int pipnet_count_encode_f32(const float* x, int B, int P, int C, int kind, int do_round,
+                            const float* w, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PIPNET_AMD_H */

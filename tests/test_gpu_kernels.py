@@ -1,0 +1,191 @@
+"""Per-kernel numerics through the C-ABI against plain PyTorch fp32/fp64 references
+(asymmetric, non-tile-multiple shapes; every epilogue; every supported channel count)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from count_pipnet_amd import _lib
+from count_pipnet_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(*shape, gen, scale=1.0):
+    return (torch.randn(*shape, generator=gen, dtype=torch.float64) * scale)
+
+
+def _gemm_tol(a, w):
+    # fp32 fma-chain error bound ~ K * eps * sum|a||w|  (loose constant)
+    return 2e-6 * (a.abs() @ w.abs().t()) + 1e-6
+
+
+@pytest.mark.parametrize("m,n,k", [(1, 1, 4), (37, 53, 48), (128, 128, 32), (300, 200, 96), (1000, 384, 1536),
+                                   (64, 6144, 2048), (2, 9, 16), (129, 257, 772)])
+def test_linear_plain(gpu, m, n, k):
+    g = torch.Generator().manual_seed(m * 7 + n * 13 + k)
+    a, w = _rand(m, k, gen=g), _rand(n, k, gen=g)
+    ref = a @ w.t()
+    out = K.linear(a.float().to(gpu), w.float().to(gpu)).double().cpu()
+    assert torch.all((out - ref).abs() <= _gemm_tol(a, w)), (out - ref).abs().max()
+
+
+def test_mfma_layout_asymmetric(gpu):
+    """A = I with an asymmetric W catches a transposed C-write (cdna guide section 3)."""
+    n = 128
+    a = torch.eye(n)
+    w = torch.arange(n * n, dtype=torch.float32).view(n, n) / 1000.0
+    out = K.linear(a.to(gpu), w.to(gpu)).cpu()
+    assert torch.equal(out, w.t().contiguous())
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_BIAS, _lib.EPI_BIAS_GELU, _lib.EPI_RESID, _lib.EPI_MUL])
+def test_linear_epilogues(gpu, epi):
+    g = torch.Generator().manual_seed(epi)
+    m, n, k = 333, 192, 384
+    a, w, b = _rand(m, k, gen=g), _rand(n, k, gen=g, scale=0.05), _rand(n, gen=g)
+    s, r = _rand(n, gen=g), _rand(m, n, gen=g)
+    acc = a @ w.t()
+    if epi == _lib.EPI_BIAS:
+        ref = acc + b
+    elif epi == _lib.EPI_BIAS_GELU:
+        ref = F.gelu(acc + b)
+    elif epi == _lib.EPI_RESID:
+        ref = r + s * (acc + b)
+    else:
+        ref = acc * r
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    out = K.linear(d(a), d(w), d(b), epi, scale=d(s), r=d(r)).double().cpu()
+    tol = 4e-6 * (1 + ref.abs()) + 4e-6 * ((a.abs() @ w.abs().t()) * (1 + s.abs() + r.abs()))
+    assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
+
+
+def test_linear_inplace_residual(gpu):
+    g = torch.Generator().manual_seed(5)
+    m, c = 700, 96
+    a, w, b, s = _rand(m, 4 * c, gen=g), _rand(c, 4 * c, gen=g, scale=0.05), _rand(c, gen=g), _rand(c, gen=g)
+    x = _rand(m, c, gen=g)
+    ref = x + s * (a @ w.t() + b)
+    xd = x.float().to(gpu)
+    K.linear(a.float().to(gpu), w.float().to(gpu), b.float().to(gpu), _lib.EPI_RESID, scale=s.float().to(gpu),
+             r=xd, out=xd)
+    assert torch.allclose(xd.double().cpu(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("cin,cout,h,stride", [(96, 192, 56, 2), (192, 384, 28, 1), (384, 768, 27, 1),
+                                               (192, 384, 28, 2), (96, 192, 9, 2)])
+def test_conv2x2(gpu, cin, cout, h, stride):
+    g = torch.Generator().manual_seed(cin + h)
+    x, w, b = _rand(3, cin, h, h, gen=g), _rand(cout, cin, 2, 2, gen=g, scale=0.05), _rand(cout, gen=g)
+    ref = F.conv2d(x, w, b, stride=stride).permute(0, 2, 3, 1)
+    xn = x.permute(0, 2, 3, 1).contiguous().float().to(gpu)
+    wp = w.permute(0, 2, 3, 1).contiguous().float().to(gpu)
+    out = K.conv2x2(xn, wp, b.float().to(gpu), stride).double().cpu()
+    assert torch.allclose(out, ref, rtol=2e-5, atol=2e-5), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("h", [224, 64, 128])
+def test_stem(gpu, h):
+    g = torch.Generator().manual_seed(h)
+    x, w, b = _rand(2, 3, h, h, gen=g), _rand(96, 3, 4, 4, gen=g, scale=0.2), _rand(96, gen=g)
+    lw, lb = 1 + 0.1 * _rand(96, gen=g), 0.1 * _rand(96, gen=g)
+    y = F.conv2d(x, w, b, stride=4).permute(0, 2, 3, 1)
+    ref = F.layer_norm(y, (96,), lw, lb, 1e-6)
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    out = K.convnext_stem(d(x), d(w), d(b), d(lw), d(lb)).double().cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-4), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("c,h", [(96, 56), (192, 28), (384, 27), (768, 26), (768, 13), (384, 14), (96, 16), (192, 8)])
+def test_dwconv7_ln(gpu, c, h):
+    g = torch.Generator().manual_seed(c + h)
+    x, w, b = _rand(2, c, h, h, gen=g), _rand(c, 1, 7, 7, gen=g, scale=0.2), _rand(c, gen=g)
+    lw, lb = 1 + 0.1 * _rand(c, gen=g), 0.1 * _rand(c, gen=g)
+    y = F.conv2d(x, w, b, padding=3, groups=c).permute(0, 2, 3, 1)
+    ref = F.layer_norm(y, (c,), lw, lb, 1e-6)
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    out = K.dwconv7_ln(d(xn), d(w.reshape(c, 49).t().contiguous()), d(b), d(lw), d(lb)).double().cpu()
+    assert torch.allclose(out, ref, rtol=1e-4, atol=1e-4), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("c", [96, 192, 384, 768, 100])
+def test_layernorm(gpu, c):
+    g = torch.Generator().manual_seed(c)
+    x, lw, lb = _rand(517, c, gen=g, scale=3.0), 1 + 0.1 * _rand(c, gen=g), 0.1 * _rand(c, gen=g)
+    ref = F.layer_norm(x, (c,), lw, lb, 1e-6)
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    out = K.layernorm(d(x), d(lw), d(lb)).double().cpu()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("p,hw,mode", [(768, 676, 0), (2048, 784, 0), (16, 64, 1), (200, 33, 0), (2048, 256, 1)])
+def test_softmax_pool(gpu, p, hw, mode):
+    g = torch.Generator().manual_seed(p + hw)
+    x = _rand(3, hw, p, gen=g, scale=4.0)
+    proto = torch.softmax(x, dim=2)
+    pooled = proto.amax(dim=1) if mode == 0 else proto.sum(dim=1)
+    pr, po = K.softmax_pool(x.float().to(gpu).view(3, hw, 1, p), mode)
+    assert torch.allclose(pr.double().cpu().view(3, hw, p), proto, rtol=1e-5, atol=1e-7)
+    assert torch.allclose(po.double().cpu(), pooled, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("thresh", [None, 0.1])
+def test_nonneg_linear(gpu, thresh):
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(64, 768, generator=g, dtype=torch.float64) * 0.3
+    w, b = _rand(200, 768, gen=g), _rand(200, gen=g)
+    xc = torch.where(x < 0.1, 0.0, x) if thresh else x
+    ref = xc @ torch.relu(w).t() + b
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    xo, out = K.nonneg_linear(d(x), d(w), d(b), thresh)
+    assert torch.equal(xo.cpu(), xc.float())
+    assert torch.allclose(out.double().cpu(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("p,hw", [(16, 64), (2048, 256), (100, 37)])
+def test_count_gumbel_injected_noise(gpu, p, hw):
+    g = torch.Generator().manual_seed(p)
+    logits = torch.randn(2, hw, p, generator=g)
+    e = torch.empty(2, p, hw).exponential_(generator=g)
+    z = logits - e.log().permute(0, 2, 1)
+    idx = z.argmax(dim=2)
+    proto, hist = K.count_gumbel(logits.to(gpu).view(2, hw, 1, p), 1.0, e.to(gpu).view(2, p, hw, 1), seed=0)
+    proto = proto.cpu().view(2, hw, p)
+    assert torch.equal(proto.argmax(dim=2), idx)
+    assert torch.all((proto.sum(dim=2) - 1).abs() <= 1.2e-7)
+    assert torch.count_nonzero(proto) == 2 * hw
+    ref_hist = torch.stack([torch.bincount(idx[i], minlength=p) for i in range(2)])
+    assert torch.equal(hist.cpu().long(), ref_hist)
+
+
+def test_count_gumbel_philox_statistics(gpu):
+    """In-kernel Philox noise: with all-zero logits the argmax is uniform over P."""
+    p, hw, b = 16, 4096, 4
+    logits = torch.zeros(b, hw, 1, p, device=gpu)
+    _, hist = K.count_gumbel(logits, 1.0, None, seed=1234)
+    h = hist.cpu().double().sum(0)
+    expected = b * hw / p
+    chi2 = float(((h - expected) ** 2 / expected).sum())
+    assert chi2 < 50.0, chi2              # 15 dof: p(chi2 > 50) ~ 1e-5
+    _, hist2 = K.count_gumbel(logits, 1.0, None, seed=1234)
+    assert torch.equal(hist, hist2)       # counter-based: reproducible per seed
+    _, hist3 = K.count_gumbel(logits, 1.0, None, seed=99)
+    assert not torch.equal(hist, hist3)
+
+
+def test_count_finish_and_encode(gpu):
+    hist = torch.tensor([[0, 1, 2, 3, 4, 7]], dtype=torch.int32, device=gpu)
+    raw, cl = K.count_finish(hist, None, 3, True)
+    assert torch.equal(cl.cpu(), torch.tensor([[0.0, 1, 2, 3, 3, 3]]))
+    sums = torch.tensor([[0.4, 0.5, 1.5, 2.5, 3.7, -0.2]], device=gpu)
+    _, cl2 = K.count_finish(None, sums, 3, True)
+    assert torch.equal(cl2.cpu(), torch.tensor([[0.0, 0.0, 2.0, 2.0, 3.0, 0.0]]))   # half to even
+    _, cl3 = K.count_finish(None, sums, 3, False)
+    assert torch.allclose(cl3.cpu(), torch.tensor([[0.4, 0.5, 1.5, 2.5, 3.0, 0.0]]))
+    x = torch.tensor([[0.0, 1.0, 3.0], [0.05, 2.0, 2.9], [1.0, 0.0, 0.2], [3.0, 2.0, 1.0]], device=gpu)
+    enc = K.count_encode(x, 3, kind=0, do_round=True).cpu().view(4, 3, 3)
+    from count_pipnet_amd.count_pipnet_utils import create_modified_encoding
+    assert torch.equal(enc, create_modified_encoding(x.cpu().round(), 3))
+    w = torch.tensor([1 / 3, 2 / 3, 1.0], device=gpu)
+    lin = K.count_encode(x, 3, kind=1, do_round=False, w=w).cpu()
+    assert torch.allclose(lin, (x.cpu().reshape(-1, 1) * w.cpu()).view(4, 9))

@@ -1,0 +1,130 @@
+"""End-to-end parity of the HIP inference path (through the C-ABI) with the reference.
+
+* every golden case recorded from the reference (tests/golden) at its recorded size;
+* the oracle (CPU restatement pinned to those goldens) on fresh seeded inputs;
+* size-independent properties at the full BASELINE size (C2: B=64, 224x224).
+
+Tolerance (BASELINE.json north star): 1e-3 fp32 on proto / pooled / logits (logits
+relative to max(1, |logit|)), argmax class indices bit-exact except where the top-2 gap
+is below that tolerance, presence flags exact except within 1e-3 of the 0.1 threshold.
+Count heads: clamped counts exact except images holding a Gumbel near-tie (< 1e-3).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import golden_args, golden_inputs, golden_names, golden_noise, golden_state_dict, load_golden, proto_shape
+from model_util import build_model
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+HIP_CASES = [n for n in golden_names() if load_golden(n)[0]["case"]["net"] != "resnet50"]
+
+
+def _check_pipnet(proto, pooled, out, r_pooled, r_out, r_proto_max, r_proto_sum, inference):
+    assert np.abs(proto.amax(axis=(2, 3)) - r_proto_max).max() <= TOL
+    assert np.abs(proto.sum(axis=(2, 3)) - r_proto_sum).max() <= TOL * max(1.0, np.abs(r_proto_sum).max())
+    near = np.abs(r_pooled - 0.1) < TOL if inference else np.zeros_like(r_pooled, dtype=bool)
+    assert np.all(np.abs(pooled - r_pooled)[~near] <= TOL)
+    scale = np.maximum(1.0, np.abs(r_out))
+    if not near.any():
+        assert np.all(np.abs(out - r_out) <= TOL * scale), np.abs(out - r_out).max()
+    srt = np.sort(r_out, axis=1)
+    decisive = (srt[:, -1] - srt[:, -2]) > 2 * TOL * scale.max(axis=1)
+    if not near.any():
+        assert np.array_equal(out.argmax(1)[decisive], r_out.argmax(1)[decisive])
+
+
+def _near_tie_images(meta, rec, margin=TOL):
+    """Images whose Gumbel argmax has a top-2 gap below ``margin`` somewhere (oracle-side)."""
+    sd, xs, args = golden_state_dict(meta), golden_inputs(meta), golden_args(meta)
+    with torch.no_grad():
+        f = ref_cpu.backbone(xs, sd, args)
+        if getattr(args, "num_features", 0):
+            f = torch.nn.functional.conv2d(f, sd["_add_on.0.weight"], sd["_add_on.0.bias"])
+        z = f - golden_noise(meta, proto_shape(meta, rec)).log()
+        top2 = z.topk(2, dim=1).values
+        return ((top2[:, 0] - top2[:, 1]) < margin).flatten(1).any(dim=1).numpy()
+
+
+@pytest.mark.parametrize("name", HIP_CASES)
+def test_hip_forward_matches_reference_golden(gpu, name):
+    meta, rec = load_golden(name)
+    net = build_model(meta).to(gpu)
+    xs = golden_inputs(meta).to(gpu)
+    count = meta["case"]["model"] == "count_pipnet"
+    gumbel = count and meta["case"]["activation"] == "gumbel_softmax"
+    if gumbel:
+        net._add_on[-1].exp_noise = golden_noise(meta, proto_shape(meta, rec)).to(gpu)
+    for inference in (True, False):
+        tag = "inf" if inference else "raw"
+        with torch.no_grad():
+            proto, pooled, out = net(xs, inference=inference)
+        torch.cuda.synchronize()
+        proto, pooled, out = proto.float().cpu().numpy(), pooled.cpu().numpy(), out.cpu().numpy()
+        if not count:
+            _check_pipnet(proto, pooled, out, rec[tag + "_pooled"], rec[tag + "_out"], rec[tag + "_proto_max"],
+                          rec[tag + "_proto_sum"], inference)
+            continue
+        ok = ~_near_tie_images(meta, rec) if gumbel else np.ones(pooled.shape[0], dtype=bool)
+        if inference:    # clamped integer counts
+            assert np.array_equal(pooled[ok], rec[tag + "_pooled"][ok])
+        else:
+            assert np.all(np.abs(pooled - rec[tag + "_pooled"])[ok] <= TOL * np.maximum(1, np.abs(rec[tag + "_pooled"][ok])))
+        scale = np.maximum(1.0, np.abs(rec[tag + "_out"][ok]))
+        assert np.all(np.abs(out[ok] - rec[tag + "_out"][ok]) <= TOL * scale), np.abs(out[ok] - rec[tag + "_out"][ok]).max()
+        if tag + "_proto" in rec:
+            assert np.all(np.abs(proto[ok] - rec[tag + "_proto"][ok]) <= TOL)
+
+
+def test_c2_full_batch_properties(gpu):
+    """C2 at its BASELINE size (bs=64, 224x224): softmax rows sum to 1, pooled is the
+    spatial max of proto, logits are the NonNegLinear of the clamped pooled vector,
+    results are batch-invariant (bitwise), and two images match the oracle."""
+    meta, _ = load_golden("c2_pipnet_convnext26")
+    net = build_model(meta).to(gpu)
+    from count_pipnet_amd.synthetic import synth_images
+    xs = synth_images(64, 224, seed=7).to(gpu)
+    with torch.no_grad():
+        proto, pooled, out = net(xs, inference=True)
+        proto3, pooled3, out3 = net(xs[5:8].contiguous(), inference=True)
+    torch.cuda.synchronize()
+    assert proto.shape == (64, 768, 26, 26) and pooled.shape == (64, 768) and out.shape == (64, 200)
+    assert torch.allclose(proto.sum(dim=1), torch.ones(64, 26, 26, device=gpu), atol=2e-6)
+    raw_max = proto.amax(dim=(2, 3))
+    assert torch.equal(pooled, torch.where(raw_max < 0.1, torch.zeros_like(raw_max), raw_max))
+    w = net._classification.weight
+    assert torch.allclose(out, pooled @ torch.relu(w).t(), rtol=1e-5, atol=1e-4)
+    assert torch.equal(proto[5:8], proto3) and torch.equal(out[5:8], out3) and torch.equal(pooled[5:8], pooled3)
+    sd = {k: v.cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        _, r_pooled, r_out = ref_cpu.pipnet_forward(xs[:2].cpu(), sd, golden_args(meta), inference=True)
+    assert (pooled[:2].cpu() - r_pooled).abs().max() <= TOL
+    assert ((out[:2].cpu() - r_out).abs() / r_out.abs().clamp(min=1)).max() <= TOL
+
+
+def test_classifier_weight_mutation_is_seen(gpu):
+    """pipnet/test.py:71-73 mutates _classification.weight in place between batches."""
+    meta, _ = load_golden("pipnet_mid_addon")
+    net = build_model(meta).to(gpu)
+    xs = golden_inputs(meta).to(gpu)
+    with torch.no_grad():
+        _, _, out1 = net(xs, inference=True)
+        net._classification.weight.copy_(torch.clamp(net._classification.weight.data - 1e-3, min=0.0))
+        _, pooled2, out2 = net(xs, inference=True)
+    assert torch.allclose(out2, pooled2 @ torch.relu(net._classification.weight).t() + net._classification.bias,
+                          rtol=1e-5, atol=1e-5)
+    assert not torch.equal(out1, out2)
+
+
+def test_backbone_weight_update_repacks(gpu):
+    meta, _ = load_golden("c1_count_identity")
+    net = build_model(meta).to(gpu)
+    net._add_on[-1].exp_noise = torch.ones(16, 16, 8, 8, device=gpu)
+    xs = golden_inputs(meta).to(gpu)
+    with torch.no_grad():
+        f1 = net._net(xs).clone()
+        net._net.features[1][0].block[0].weight.mul_(0.5)     # depthwise weight is repacked
+        f2 = net._net(xs)
+    assert not torch.equal(f1, f2)
