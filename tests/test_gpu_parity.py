@@ -23,7 +23,7 @@ HIP_CASES = [n for n in golden_names() if load_golden(n)[0]["case"]["net"] != "r
 
 
 def _check_pipnet(proto, pooled, out, r_pooled, r_out, r_proto_max, r_proto_sum, inference):
-    assert np.abs(proto.amax(axis=(2, 3)) - r_proto_max).max() <= TOL
+    assert np.abs(proto.max(axis=(2, 3)) - r_proto_max).max() <= TOL
     assert np.abs(proto.sum(axis=(2, 3)) - r_proto_sum).max() <= TOL * max(1.0, np.abs(r_proto_sum).max())
     near = np.abs(r_pooled - 0.1) < TOL if inference else np.zeros_like(r_pooled, dtype=bool)
     assert np.all(np.abs(pooled - r_pooled)[~near] <= TOL)

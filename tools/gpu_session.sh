@@ -1,0 +1,22 @@
+#!/bin/bash
+# One GPU-box session: gpu tests -> smoke -> bench -> rocprof kernel summary.
+# Test failures (exit 1) do not stop the session; faults, aborts and time limits do.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+stop_if_fatal() {  # $1 = exit code, $2 = step name
+  local rc=$1
+  echo "[$2] exit $rc" | tee -a gpurun_out/session.log
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "fatal exit in $2; stopping" | tee -a gpurun_out/session.log; exit "$rc"; fi
+}
+STEPS="${STEPS:-tests smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests) timeout -k 10 900 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; stop_if_fatal $? tests; tail -30 gpurun_out/pytest_gpu.log ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1; stop_if_fatal $? smoke; tail -3 gpurun_out/smoke.log ;;
+    bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; stop_if_fatal $? bench; tail -3 gpurun_out/bench.log ;;
+    prof)  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1); stop_if_fatal $? prof; find gpurun_out/prof -name "*stats*" | head ;;
+  esac
+done
+exit 0
