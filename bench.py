@@ -177,7 +177,7 @@ def main():
                                "(BASELINE configs[1]; configs[3] at N=8)",
                    "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
                    "parallelism": f"dp{world}", "exchange": "rccl all_gather(logits, pooled)" if world > 1 else None},
-        "roofline": {"bound": "mfma", "kernel": f"(anonymous namespace)::gemm_f32_tn_kernel<{dom[19:-1]}>",
+        "roofline": {"bound": "mfma", "kernel": dom,
                      "achieved": fl / tt / 1e12, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
                      "frac": fl / tt / 1e12 / PEAK_F32_TFLOPS, "traffic": None,
                      "launches_per_step": n_l / a.steps, "avg_launch_us": tt / n_l * 1e6,

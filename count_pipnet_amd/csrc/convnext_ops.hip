@@ -11,69 +11,71 @@ namespace {
 constexpr float LN_EPS = 1e-6f;
 
 // ---------------------------------------------------------------------------------------
-// stem: one workgroup per (image, output row); thread = (pixel, 24-channel group).
+// stem: one workgroup per (image, output row).  Input rows and transposed weights in LDS;
+// thread = (4-channel quad, pixel group), float4 accumulators; the raw row goes back through
+// LDS for the LayerNorm (one wave per pixel) so the NHWC row is written fully coalesced.
 // ---------------------------------------------------------------------------------------
-constexpr int STEM_C = 96, STEM_K = 48, STEM_WLD = 49;
+constexpr int STEM_C = 96, STEM_K = 48, STEM_Q = STEM_C / 4, STEM_G = 10, STEM_NPX = 6;
+constexpr int STEM_OLD = STEM_C + 4;       // padded LDS row of the raw output tile
 
 __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W,
                                                    const float* __restrict__ w, const float* __restrict__ bias,
                                                    const float* __restrict__ lnw, const float* __restrict__ lnb,
                                                    float* __restrict__ y) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* wsm = sm;                                 // [96][49]
-  float* xin = sm + STEM_C * STEM_WLD;             // [3][4][W]
   const int OH = H / 4, OW = W / 4;
+  float* wsm = sm;                                 // [48][96]  (k-major: float4 over channels)
+  float* otile = wsm + STEM_K * STEM_C;            // [OW][100]
+  float* xin = otile + OW * STEM_OLD;              // [3][4][W]
   const int b = blockIdx.x / OH, oy = blockIdx.x - (blockIdx.x / OH) * OH;
   const int tid = threadIdx.x;
-  for (int i = tid; i < STEM_C * STEM_K; i += 256) wsm[(i / STEM_K) * STEM_WLD + i % STEM_K] = w[i];
-  for (int i = tid; i < 12 * W; i += 256) {
-    const int c = i / (4 * W), r = i - c * 4 * W, ky = r / W, xx = r - ky * W;
-    xin[i] = x[(((int64_t)b * 3 + c) * H + 4 * oy + ky) * W + xx];
+  for (int i = tid; i < STEM_C * STEM_K; i += 256) {
+    const int c = i / STEM_K, k = i - c * STEM_K;
+    wsm[k * STEM_C + c] = w[i];
+  }
+  const int w4 = W / 4;
+  for (int i = tid; i < 12 * w4; i += 256) {
+    const int r = i / w4, xx = i - r * w4;          // r = c*4 + ky
+    const int c = r >> 2, ky = r & 3;
+    st4(xin + r * W + 4 * xx, ld4(x + (((int64_t)b * 3 + c) * H + 4 * oy + ky) * W + 4 * xx));
   }
   __syncthreads();
-  const int cg = tid & 3;
-  for (int px = tid >> 2; px < OW; px += 64) {
-    float in[STEM_K];
+  const int q = tid % STEM_Q, g = tid / STEM_Q;
+  if (g < STEM_G) {
+    const f32x4 bq = ld4(bias + 4 * q);
+    for (int px0 = g; px0 < OW; px0 += STEM_G * STEM_NPX) {
+      f32x4 acc[STEM_NPX];
 #pragma unroll
-    for (int c = 0; c < 3; ++c)
+      for (int p = 0; p < STEM_NPX; ++p) acc[p] = bq;
+#pragma unroll 4
+      for (int k = 0; k < STEM_K; ++k) {
+        const f32x4 wk = ld4(wsm + k * STEM_C + 4 * q);
+        const float* xr = xin + (k >> 2) * W + (k & 3);   // (c*4+ky) row, kx column offset
 #pragma unroll
-      for (int ky = 0; ky < 4; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 4; ++kx) in[c * 16 + ky * 4 + kx] = xin[(c * 4 + ky) * W + 4 * px + kx];
-    float o[24];
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const int co = cg * 24 + j;
-      float a = bias[co];
-#pragma unroll
-      for (int k = 0; k < STEM_K; ++k) a = fmaf(wsm[co * STEM_WLD + k], in[k], a);
-      o[j] = a;
-      s += a;
-    }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    const float mean = s * (1.0f / STEM_C);
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < 24; ++j) {
-      const float d = o[j] - mean;
-      q = fmaf(d, d, q);
-    }
-    q += __shfl_xor(q, 1, 64);
-    q += __shfl_xor(q, 2, 64);
-    const float rstd = 1.0f / sqrtf(q * (1.0f / STEM_C) + LN_EPS);
-    float* dst = y + (((int64_t)b * OH + oy) * OW + px) * STEM_C + cg * 24;
-#pragma unroll
-    for (int j = 0; j < 24; j += 4) {
-      f32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int co = cg * 24 + j + e;
-        v[e] = (o[j + e] - mean) * rstd * lnw[co] + lnb[co];
+        for (int p = 0; p < STEM_NPX; ++p) {
+          const int px = px0 + p * STEM_G;
+          const float v = px < OW ? xr[4 * px] : 0.f;
+          acc[p] += v * wk;
+        }
       }
-      st4(dst + j, v);
+#pragma unroll
+      for (int p = 0; p < STEM_NPX; ++p) {
+        const int px = px0 + p * STEM_G;
+        if (px < OW) st4(otile + px * STEM_OLD + 4 * q, acc[p]);
+      }
     }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int px = wv; px < OW; px += 4) {
+    const float v0 = otile[px * STEM_OLD + lane];
+    const float v1 = lane < 32 ? otile[px * STEM_OLD + 64 + lane] : 0.f;
+    const float mean = wave_sum(v0 + v1) * (1.0f / STEM_C);
+    const float d0 = v0 - mean, d1 = lane < 32 ? v1 - mean : 0.f;
+    const float rstd = 1.0f / sqrtf(wave_sum(d0 * d0 + d1 * d1) * (1.0f / STEM_C) + LN_EPS);
+    float* dst = y + (((int64_t)b * OH + oy) * OW + px) * STEM_C;
+    dst[lane] = d0 * rstd * lnw[lane] + lnb[lane];
+    if (lane < 32) dst[64 + lane] = d1 * rstd * lnw[64 + lane] + lnb[64 + lane];
   }
 }
 
@@ -100,8 +102,13 @@ __global__ __launch_bounds__(DW_THREADS) void dwconv7_ln_kernel(const float* __r
 
   const int tid = threadIdx.x;
   const int q = tid % QC, g = tid / QC;
-  const int b = blockIdx.z, oy = blockIdx.y;
-  const int xblk = blockIdx.x * NP;
+  // 1-D grid, XCD-contiguous: the 7-row halo of neighbouring output rows is served by one L2
+  const int nxb = (W + NP - 1) / NP;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int xb = lin % nxb;
+  const int oy = (lin / nxb) % H;
+  const int b = lin / (nxb * H);
+  const int xblk = xb * NP;
   const int px0 = xblk + g * TX;
 
   const f32x4 bq = ld4(bias + 4 * q);
@@ -165,7 +172,7 @@ template <int C, int TX>
 int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
               const float* lnb, float* y, hipStream_t s) {
   constexpr int NP = (DW_THREADS / (C / 4)) * TX;
-  const dim3 grid((W + NP - 1) / NP, H, B);
+  const dim3 grid(((W + NP - 1) / NP) * H * B);
   hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw, lnb, y);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
@@ -211,11 +218,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 
 extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, const float* w, const float* b,
                                         const float* ln_w, const float* ln_b, float* y, void* stream) {
-  if (B < 0 || H < 4 || W < 4 || (H & 3) || (W & 3) || W > 4096) return PIPNET_ERR_ARG;
+  if (B < 0 || H < 4 || W < 4 || (H & 3) || (W & 3) || W > 960) return PIPNET_ERR_ARG;
   if (!x || !w || !b || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
-  if (!aligned16(y)) return PIPNET_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(y) || !aligned16(b)) return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
-  const size_t shmem = (STEM_C * STEM_WLD + 12 * W) * sizeof(float);
+  const size_t shmem = (STEM_K * STEM_C + (W / 4) * STEM_OLD + 12 * W) * sizeof(float);
   hipLaunchKernelGGL(stem_kernel, dim3(B * (H / 4)), dim3(256), shmem, (hipStream_t)stream, x, H, W, w, b, ln_w,
                      ln_b, y);
   PIPNET_CHECK_LAUNCH();

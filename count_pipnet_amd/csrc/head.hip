@@ -73,30 +73,52 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const float*
 }
 
 // ---------------------------------------------------------------------------------------
-// NonNegLinear: one workgroup per image, x' staged in LDS, one wave per output class.
+// NonNegLinear: grid (image, class block of 16); x' staged in LDS; each wave computes 4
+// classes at once (4 independent dot products in flight, float4 W reads).
 // ---------------------------------------------------------------------------------------
+constexpr int NN_CLS_PER_BLOCK = 16;
+
 __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float* __restrict__ x, int D,
                                                                      const float* __restrict__ W,
                                                                      const float* __restrict__ bias, int K,
                                                                      int apply_thresh, float thresh,
                                                                      float* __restrict__ x_out,
                                                                      float* __restrict__ out) {
-  extern __shared__ float xs[];
+  extern __shared__ __attribute__((aligned(16))) float xs[];
   const int b = blockIdx.x;
   for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
     float v = x[(int64_t)b * D + c];
     if (apply_thresh && v < thresh) v = 0.f;
     xs[c] = v;
-    if (x_out) x_out[(int64_t)b * D + c] = v;
+    if (x_out && blockIdx.y == 0) x_out[(int64_t)b * D + c] = v;
   }
   __syncthreads();
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int k = wv; k < K; k += HEAD_THREADS / 64) {
+  const int k0 = blockIdx.y * NN_CLS_PER_BLOCK + wv * 4;
+  const bool vec = (D & 3) == 0;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + j;
+    if (k >= K) break;
     const float* wr = W + (int64_t)k * D;
-    float s = 0.f;
-    for (int c = lane; c < D; c += 64) s = fmaf(xs[c], fmaxf(wr[c], 0.f), s);
-    s = wave_sum(s);
-    if (lane == 0) out[(int64_t)b * K + k] = s + (bias ? bias[k] : 0.f);
+    if (vec) {
+      for (int c = 4 * lane; c < D; c += 256) {
+        const f32x4 wv4 = ld4(wr + c), xv = ld4(xs + c);
+        s[j] = fmaf(xv[0], fmaxf(wv4[0], 0.f), s[j]);
+        s[j] = fmaf(xv[1], fmaxf(wv4[1], 0.f), s[j]);
+        s[j] = fmaf(xv[2], fmaxf(wv4[2], 0.f), s[j]);
+        s[j] = fmaf(xv[3], fmaxf(wv4[3], 0.f), s[j]);
+      }
+    } else {
+      for (int c = lane; c < D; c += 64) s[j] = fmaf(xs[c], fmaxf(wr[c], 0.f), s[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = k0 + j;
+    const float t = wave_sum(s[j]);
+    if (lane == 0 && k < K) out[(int64_t)b * K + k] = t + (bias ? bias[k] : 0.f);
   }
 }
 
@@ -258,7 +280,9 @@ extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const floa
                                         int apply_thresh, float thresh, float* x_out, float* out, void* stream) {
   if (B < 0 || D <= 0 || K <= 0 || D > 16384 || !x || !W || !out) return PIPNET_ERR_ARG;
   if (B == 0) return PIPNET_OK;
-  hipLaunchKernelGGL(nonneg_linear_kernel, dim3(B), dim3(HEAD_THREADS), sizeof(float) * D, (hipStream_t)stream, x,
+  if ((D & 3) == 0 && (!aligned16(W) || !aligned16(x))) return PIPNET_ERR_ALIGN;
+  const dim3 grid(B, (K + NN_CLS_PER_BLOCK - 1) / NN_CLS_PER_BLOCK);
+  hipLaunchKernelGGL(nonneg_linear_kernel, grid, dim3(HEAD_THREADS), sizeof(float) * D, (hipStream_t)stream, x,
                      D, W, bias, K, apply_thresh, thresh, x_out, out);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;

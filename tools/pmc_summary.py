@@ -1,0 +1,52 @@
+"""Summarise tools/pmc.sh output: per kernel, average duration, effective clock, MFMA busy,
+HBM bytes per launch (FETCH_SIZE doubled for the gfx950 wide-read undercount, KB units),
+and write profiles/traffic_latest.json for bench.py's roofline.traffic field."""
+import csv
+import glob
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+d = sys.argv[1]
+
+
+def load(pass_dir):
+    rows = []
+    for f in glob.glob(os.path.join(d, pass_dir, "**", "*counter_collection.csv"), recursive=True):
+        rows += list(csv.DictReader(open(f)))
+    return rows
+
+
+def short(name):
+    m = re.search(r"(\w+)(<[^>]*>)?\(", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+
+
+agg = defaultdict(lambda: defaultdict(list))
+for p in ("p1", "p2", "p3"):
+    for r in load(p):
+        k = short(r.get("Kernel_Name", ""))
+        agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if "Start_Timestamp" in r and "End_Timestamp" in r and r["Counter_Name"] in ("GRBM_GUI_ACTIVE", "FETCH_SIZE"):
+            agg[k]["dur_ns_" + p].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
+
+out = {}
+print(f"{'kernel':48s} {'n':>4s} {'dur_us':>8s} {'clk_GHz':>8s} {'mfma_busy':>9s} {'rd_MB':>9s} {'wr_MB':>9s}")
+for k, c in sorted(agg.items(), key=lambda kv: -sum(kv[1].get("dur_ns_p1", [0]))):
+    n = len(c.get("GRBM_GUI_ACTIVE", [])) or 1
+    dur = sum(c.get("dur_ns_p1", [0])) / max(1, len(c.get("dur_ns_p1", [])))
+    grbm = sum(c.get("GRBM_GUI_ACTIVE", [0])) / n
+    clk = grbm / 8 / dur if dur else 0.0          # GRBM_GUI_ACTIVE summed over 8 XCDs (cycles)
+    busy = sum(c.get("SQ_BUSY_CYCLES", [0])) / n
+    mf = sum(c.get("SQ_VALU_MFMA_BUSY_CYCLES", [0])) / n
+    nf = len(c.get("FETCH_SIZE", [])) or 1
+    nw = len(c.get("WRITE_SIZE", [])) or 1
+    rd = 2 * sum(c.get("FETCH_SIZE", [0])) / nf * 1024      # KB -> B, x2 gfx950 wide-read correction
+    wr = sum(c.get("WRITE_SIZE", [0])) / nw * 1024
+    mfu = mf / (grbm / 8 * 256 * 4) if grbm else 0.0        # per-SIMD busy fraction (cycles units)
+    print(f"{k:48s} {n:4d} {dur / 1e3:8.1f} {clk:8.2f} {mfu:9.3f} {rd / 1e6:9.1f} {wr / 1e6:9.1f}")
+    out[k] = dict(launches=n, avg_us=dur / 1e3, clock_ghz=clk, mfma_busy=mfu, sq_busy=busy,
+                  hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes=rd + wr)
+json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
