@@ -1,0 +1,117 @@
+// depthwise 7x7 + LayerNorm(C) kernel template (shared by convnext_ops.hip and tools/dw_lab.hip)
+#pragma once
+#include "common.hpp"
+
+namespace pipnet_dw {
+
+constexpr float LN_EPS = 1e-6f;
+constexpr int DW_THREADS = 192;
+
+// 192 threads = G groups x (C/4) channel quads; group g computes a TY x TX tile of output
+// pixels (TY rows, TX consecutive columns).  Each input row of the 7-row halo is loaded
+// once into registers (TX+6 float4) and feeds every output row it touches; the raw tile
+// then goes through LDS for the per-pixel LayerNorm (one wave per pixel, two-pass
+// mean / variance, coalesced NHWC stores).  1-D grid, XCD-contiguous, so the halo rows of
+// neighbouring workgroups are served from one L2.
+template <int C, int TX, int TY, int MINB>
+__global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
+                                                                      const float* __restrict__ wp,
+                                                                      const float* __restrict__ bias,
+                                                                      const float* __restrict__ lnw,
+                                                                      const float* __restrict__ lnb,
+                                                                      float* __restrict__ y) {
+  constexpr int QC = C / 4;
+  constexpr int G = DW_THREADS / QC;
+  constexpr int NP = G * TX;
+  constexpr int NJ = (C + 63) / 64;
+  __shared__ __attribute__((aligned(16))) float tile[TY * NP * C];
+
+  const int tid = threadIdx.x;
+  const int q = tid % QC, g = tid / QC;
+  const int nxb = (W + NP - 1) / NP;
+  const int nyb = (H + TY - 1) / TY;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int xb = lin % nxb;
+  const int oy0 = ((lin / nxb) % nyb) * TY;
+  const int b = lin / (nxb * nyb);
+  const int xblk = xb * NP;
+  const int px0 = xblk + g * TX;
+
+  const f32x4 bq = ld4(bias + 4 * q);
+  f32x4 acc[TY][TX];
+#pragma unroll
+  for (int t = 0; t < TY; ++t)
+#pragma unroll
+    for (int i = 0; i < TX; ++i) acc[t][i] = bq;
+
+#pragma unroll
+  for (int ir = 0; ir < TY + 6; ++ir) {
+    const int iy = oy0 + ir - 3;
+    if (iy < 0 || iy >= H) continue;
+    const float* row = x + (((int64_t)b * H + iy) * W) * C + 4 * q;
+    f32x4 v[TX + 6];
+#pragma unroll
+    for (int r = 0; r < TX + 6; ++r) {
+      const int ix = px0 + r - 3;
+      v[r] = (ix >= 0 && ix < W) ? ld4(row + (int64_t)ix * C) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int t = 0; t < TY; ++t) {
+      const int ky = ir - t;
+      if (ky < 0 || ky >= 7) continue;
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) {
+        const f32x4 wk = ld4(wp + (ky * 7 + kx) * C + 4 * q);
+#pragma unroll
+        for (int px = 0; px < TX; ++px) acc[t][px] += v[px + kx] * wk;
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < TY; ++t)
+#pragma unroll
+    for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
+  __syncthreads();
+
+  const int lane = tid & 63, wv = tid >> 6;
+  for (int pp = wv; pp < TY * NP; pp += DW_THREADS / 64) {
+    const int t = pp / NP, pix = pp - t * NP;
+    const int ox = xblk + pix, oy = oy0 + t;
+    if (ox >= W || oy >= H) continue;
+    float vv[NJ];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      vv[j] = (c < C) ? tile[pp * C + c] : 0.f;
+      s += vv[j];
+    }
+    const float mean = wave_sum(s) * (1.0f / C);
+    float qq = 0.f;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      const float d = (c < C) ? vv[j] - mean : 0.f;
+      qq = fmaf(d, d, qq);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
+    float* dst = y + (((int64_t)b * H + oy) * W + ox) * C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) dst[c] = (vv[j] - mean) * rstd * lnw[c] + lnb[c];
+    }
+  }
+}
+
+template <int C, int TX, int TY, int MINB>
+inline int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
+                     const float* lnb, float* y, hipStream_t s) {
+  constexpr int NP = (DW_THREADS / (C / 4)) * TX;
+  const dim3 grid(((W + NP - 1) / NP) * ((H + TY - 1) / TY) * B);
+  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX, TY, MINB>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw,
+                     lnb, y);
+  return hipGetLastError() == hipSuccess ? PIPNET_OK : PIPNET_ERR_LAUNCH;
+}
+
+}  // namespace pipnet_dw

@@ -5,6 +5,7 @@
 // torchvision semantics restated in SURVEY.md 2.3; the reference builds the net in
 // features/convnext_features.py:38-94.
 #include "common.hpp"
+#include "convnext_dw.hpp"
 
 namespace {
 
@@ -80,105 +81,6 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
 }
 
 // ---------------------------------------------------------------------------------------
-// depthwise 7x7 + LayerNorm(C).  192 threads = G groups x (C/4) channel quads; group g
-// computes TX consecutive pixels of one output row with a sliding 7-column window held
-// in registers, then the row tile goes through LDS for the per-pixel LayerNorm (one
-// wave per pixel, two-pass mean / variance).
-// ---------------------------------------------------------------------------------------
-constexpr int DW_THREADS = 192;
-
-template <int C, int TX>
-__global__ __launch_bounds__(DW_THREADS) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
-                                                                const float* __restrict__ wp,
-                                                                const float* __restrict__ bias,
-                                                                const float* __restrict__ lnw,
-                                                                const float* __restrict__ lnb,
-                                                                float* __restrict__ y) {
-  constexpr int QC = C / 4;
-  constexpr int G = DW_THREADS / QC;
-  constexpr int NP = G * TX;
-  constexpr int NJ = (C + 63) / 64;
-  __shared__ __attribute__((aligned(16))) float tile[NP * C];
-
-  const int tid = threadIdx.x;
-  const int q = tid % QC, g = tid / QC;
-  // 1-D grid, XCD-contiguous: the 7-row halo of neighbouring output rows is served by one L2
-  const int nxb = (W + NP - 1) / NP;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int xb = lin % nxb;
-  const int oy = (lin / nxb) % H;
-  const int b = lin / (nxb * H);
-  const int xblk = xb * NP;
-  const int px0 = xblk + g * TX;
-
-  const f32x4 bq = ld4(bias + 4 * q);
-  f32x4 acc[TX];
-#pragma unroll
-  for (int i = 0; i < TX; ++i) acc[i] = bq;
-
-  for (int ky = 0; ky < 7; ++ky) {
-    const int iy = oy + ky - 3;
-    if (iy < 0 || iy >= H) continue;
-    const float* row = x + (((int64_t)b * H + iy) * W) * C + 4 * q;
-    f32x4 wk[7];
-#pragma unroll
-    for (int kx = 0; kx < 7; ++kx) wk[kx] = ld4(wp + (ky * 7 + kx) * C + 4 * q);
-#pragma unroll
-    for (int r = 0; r < TX + 6; ++r) {
-      const int ix = px0 + r - 3;
-      const f32x4 v = (ix >= 0 && ix < W) ? ld4(row + (int64_t)ix * C) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kx = 0; kx < 7; ++kx) {
-        const int px = r - kx;
-        if (px >= 0 && px < TX) acc[px] += v * wk[kx];
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TX; ++i) st4(tile + (g * TX + i) * C + 4 * q, acc[i]);
-  __syncthreads();
-
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int pix = wv; pix < NP; pix += DW_THREADS / 64) {
-    const int ox = xblk + pix;
-    if (ox >= W) break;
-    float v[NJ];
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      v[j] = (c < C) ? tile[pix * C + c] : 0.f;
-      s += v[j];
-    }
-    const float mean = wave_sum(s) * (1.0f / C);
-    float qq = 0.f;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      const float d = (c < C) ? v[j] - mean : 0.f;
-      qq = fmaf(d, d, qq);
-    }
-    const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
-    float* dst = y + (((int64_t)b * H + oy) * W + ox) * C;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      if (c < C) dst[c] = (v[j] - mean) * rstd * lnw[c] + lnb[c];
-    }
-  }
-}
-
-template <int C, int TX>
-int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
-              const float* lnb, float* y, hipStream_t s) {
-  constexpr int NP = (DW_THREADS / (C / 4)) * TX;
-  const dim3 grid(((W + NP - 1) / NP) * H * B);
-  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw, lnb, y);
-  PIPNET_CHECK_LAUNCH();
-  return PIPNET_OK;
-}
-
-// ---------------------------------------------------------------------------------------
 // row LayerNorm: one wave per row of C channels.
 // ---------------------------------------------------------------------------------------
 template <int NJ>
@@ -238,10 +140,10 @@ extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C,
   if (B == 0) return PIPNET_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
-    case 96: return launch_dw<96, 7>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
-    case 192: return launch_dw<192, 7>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
-    case 384: return launch_dw<384, 14>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
-    case 768: return launch_dw<768, 13>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 192: return pipnet_dw::launch_dw<192, 7, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 384: return pipnet_dw::launch_dw<384, 7, 1, 2>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 768: return pipnet_dw::launch_dw<768, 13, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     default: return PIPNET_ERR_ARG;
   }
 }

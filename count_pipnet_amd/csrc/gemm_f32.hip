@@ -13,24 +13,39 @@ int choose_group_m(const GemmParams& p) {
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 
-// K-tile depth (measured with tools/gemm_lab.py on the network's shapes, MI355X):
-// BK=16 (32 KiB LDS, 4 workgroups/CU) wins +5..+28 % on short reductions (K <= 384) and
-// on narrow outputs (N <= 192); BK=32 (64 KiB, 2 workgroups/CU) wins +2..+7 % on the
-// long K=768..3072 reductions of stages 3-4.
+// Variant selection (measured with tools/gemm_lab.py on the network's shapes, MI355X,
+// float4 epilogue, profiles/r01/gemm_lab_*.txt):
+//   K <= 96, N > 192          BK=16, 128-row tiles, 3 LDS stages      (+11 % on stage-1 fc1)
+//   N <= 384 or K <= 192      BK=32,  64-row tiles, 3 workgroups/CU   (+5..+8 %: shallow grids)
+//   or M <= 64
+//   otherwise                 BK=32, 128-row tiles, 2 LDS stages      (stage-3/4 fc1, fc2)
+// 0 = register-staged K-tail kernel, 1 = BK16x128 rows x3 stages, 2 = BK32x64 rows,
+// 3 = BK32x128 rows (mirrored by count_pipnet_amd/kernels.py:gemm_kernel_name)
+int gemm_variant(int M, int N, int K, bool vec) {
+  if (!vec) return 0;
+  if (K % 16 == 0 && K <= 96 && N > 192 && M > 64) return 1;
+  if (K % 32) return K % 16 == 0 && M > 64 ? 1 : 0;
+  if (N <= 384 || K <= 192 || M <= 64) return 2;
+  return 3;
+}
+
 template <int ALOAD>
 int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
-  p.mt = (p.M + BM - 1) / BM;
   p.nt = (p.N + BN - 1) / BN;
   p.group_m = choose_group_m(p);
-  const dim3 grid(p.mt * p.nt), block(NTHREADS);
+  p.vec_epi = (p.N % 4 == 0) && (p.ldc % 4 == 0) && aligned16(p.C) &&
+              (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
+              (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD == ALOAD_CONV2X2 || (p.lda & 3) == 0);
-  const bool bk32 = vec && (p.K % 32) == 0 && p.K > 384 && p.N > 192;
-  const bool bk16 = vec && !bk32 && (p.K % 16) == 0;
-#define PIPNET_EPI_CASE(E)                                                                          \
-  case E:                                                                                          \
-    if (bk32) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, E, ALOAD, 2>), grid, block, 0, s, p);      \
-    else if (bk16) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, E, ALOAD, 4>), grid, block, 0, s, p); \
-    else hipLaunchKernelGGL((gemm_f32_tn_ktail_kernel<E, ALOAD>), grid, block, 0, s, p);            \
+  const int v = gemm_variant(p.M, p.N, p.K, vec);
+  p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
+  const dim3 grid(p.mt * p.nt), block(NTHREADS);
+#define PIPNET_EPI_CASE(E)                                                                                 \
+  case E:                                                                                                 \
+    if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
+    else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2>), grid, block, 0, s, p); \
+    else if (v == 3) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 2, E, ALOAD, 2, 2>), grid, block, 0, s, p); \
+    else hipLaunchKernelGGL((gemm_f32_tn_ktail_kernel<E, ALOAD>), grid, block, 0, s, p);                   \
     break;
   switch (epi) {
     PIPNET_EPI_CASE(PIPNET_EPI_NONE)

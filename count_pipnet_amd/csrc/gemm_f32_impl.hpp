@@ -8,28 +8,28 @@
 // operands are K-contiguous in HBM (NHWC activations [M][K], torch Linear weights [N][K]),
 // so one kernel serves them all; the A-tile loader is the only thing that differs.
 //
-// Tile: 128x128xBK per 256-thread workgroup, 4 waves in 2x2, each wave 64x64 = 2x2 MFMA
-// 32x32 tiles (64 accumulator VGPRs).  For v_mfma_f32_32x32x2_f32 lane l supplies
-// A[l&31][k] and B[k][l&31] with k = l>>5 of the 2-deep step; the k order inside a
-// BK-deep LDS tile is free (both operands use the same map), so half-wave h walks
-// k = h*BK/2 .. (h+1)*BK/2-1 and reads its operands 4 k-steps at a time (ds_read_b128).
+// Tile: (64*TM)x128xBK per 256-thread workgroup, 4 waves in 2x2, each wave (32*TM)x64 =
+// TMx2 MFMA 32x32 tiles.  For v_mfma_f32_32x32x2_f32 lane l supplies A[l&31][k] and
+// B[k][l&31] with k = l>>5 of the 2-deep step; the k order inside a BK-deep LDS tile is
+// free (both operands use the same map), so half-wave h walks k = h*BK/2 .. (h+1)*BK/2-1
+// and reads its operands 4 k-steps at a time (ds_read_b128).  TM=1 (64-row tiles) halves
+// the tail of grids that are only ~2-3 workgroups deep per CU.
 //
 // Main path (K % BK == 0): global -> LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per
-// wave instruction), two LDS buffers, one barrier per K-tile.  LDS rows are BK*4 bytes
-// with the 16-B chunk index XOR-swizzled by a row-dependent mask: the DMA writes
-// lane-linear, so the swizzle is applied to each lane's SOURCE address and undone on the
-// read (cdna_hip_programming.md rule 21); every ds_read_b128 lane group then hits 16
-// distinct 16-B bank slots.  Operand fragments are software-pipelined in two named
-// register sets, and the first fragment group of tile k+1 is read right after the
-// barrier, under the last MFMA group of tile k.  BK=16 keeps a workgroup at 32 KiB of
-// LDS and 128 VGPRs so four workgroups (16 waves) share a CU and hide the DMA latency.
+// wave instruction), NS LDS stages, one barrier per K-tile.  LDS rows are BK*4 bytes with
+// the 16-B chunk index XOR-swizzled by a row-dependent mask: the DMA writes lane-linear,
+// so the swizzle is applied to each lane's SOURCE address and undone on the read
+// (cdna_hip_programming.md rule 21); every ds_read_b128 lane group then hits 16 distinct
+// 16-B bank slots.  Operand fragments are software-pipelined in two named register sets,
+// and the first fragment group of tile k+1 is read right after the barrier, under the last
+// MFMA group of tile k.
 // General path (any K % 4): register staging with zero-fill of the K tail.
 #pragma once
 #include "common.hpp"
 
 namespace pipnet_gemm {
 
-constexpr int BM = 128, BN = 128, NTHREADS = 256, NWAVES = 4;
+constexpr int BN = 128, NTHREADS = 256, NWAVES = 4;
 
 struct GemmParams {
   const float* A;
@@ -45,6 +45,7 @@ struct GemmParams {
   // implicit conv2x2 A-loader
   int H, Wd, Cin, OH, OW, stride;
   int mt, nt, group_m;
+  int vec_epi;     // 1: float4 epilogue through LDS (N, ldc, ldr % 4 == 0, C / R 16-B aligned)
 };
 
 enum { ALOAD_DENSE = 0, ALOAD_CONV2X2 = 1 };
@@ -88,9 +89,11 @@ PIPNET_DEV float gelu_fast(float x) {
   return x * (x < 0.f ? half_erfc : 1.0f - half_erfc);
 }
 
-template <int EPI>
-PIPNET_DEV void epilogue(const GemmParams& p, const f32x16 (&acc)[2][2], int m0, int n0, int wm, int wn, int lr,
-                         int lh) {
+using Acc = f32x16[2][2];
+
+// scalar epilogue (any N / ldc): lane owns column n, rows (v&3) + 8(v>>2) + 4h per tile
+template <int EPI, int TM>
+PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, int wm, int wn, int lr, int lh) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + j * 32 + lr;
@@ -100,10 +103,10 @@ PIPNET_DEV void epilogue(const GemmParams& p, const f32x16 (&acc)[2][2], int m0,
       bn = p.bias ? p.bias[n] : 0.f;
     if (EPI == PIPNET_EPI_RESID) sn = p.scale ? p.scale[n] : 1.f;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
-        const int m = m0 + wm * 64 + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
+        const int m = m0 + wm * 32 * TM + i * 32 + (v & 3) + 8 * (v >> 2) + 4 * lh;
         if (m >= p.M) continue;
         float x = acc[i][j][v];
         if (EPI == PIPNET_EPI_BIAS) x = x + bn;
@@ -116,8 +119,68 @@ PIPNET_DEV void epilogue(const GemmParams& p, const f32x16 (&acc)[2][2], int m0,
   }
 }
 
+template <int EPI>
+PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4& r) {
+  if (EPI == PIPNET_EPI_BIAS) x = x + bn;
+  if (EPI == PIPNET_EPI_BIAS_GELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = gelu_fast(x[e] + bn[e]);
+  }
+  if (EPI == PIPNET_EPI_RESID) x = r + sn * (x + bn);
+  if (EPI == PIPNET_EPI_MUL) x = x * r;
+  return x;
+}
+
+// Vectorised epilogue: each wave re-lays its accumulator tile through LDS (32 rows at a
+// time, 8 KiB per wave) so every global store / residual load is a float4 and one wave
+// instruction covers 4 rows x 256 B -- the lane-per-column MFMA layout would otherwise
+// cost 64 scattered dword stores (and loads) per lane, which measured as long as the
+// whole main loop on the K=96 GEMMs.  All residual float4 loads of a lane are issued
+// before the first store (one latency, not sixteen).  Needs N % 4 == 0, ldc / ldr % 4 ==
+// 0, 16-B aligned C / R, and 32 KiB of the kernel's LDS (free after the main loop).
+template <int EPI, int TM>
+PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, int m0, int n0, int wm, int wn,
+                             int lane, int wid) {
+  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL;
+  float* wt = smem + wid * 32 * 64;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int c4 = lane & 15;
+  const int n = n0 + wn * 64 + 4 * c4;
+  const bool nok = n < p.N;
+  f32x4 bn = {0.f, 0.f, 0.f, 0.f}, sn = {1.f, 1.f, 1.f, 1.f};
+  if ((EPI == PIPNET_EPI_BIAS || EPI == PIPNET_EPI_BIAS_GELU || EPI == PIPNET_EPI_RESID) && p.bias && nok)
+    bn = ld4(p.bias + n);
+  if (EPI == PIPNET_EPI_RESID && p.scale && nok) sn = ld4(p.scale + n);
+  f32x4 r[TM][8];
+  if (HAS_R) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int m = min(m0 + wm * 32 * TM + i * 32 + it * 4 + (lane >> 4), p.M - 1);
+        r[i][it] = nok ? ld4(p.R + (int64_t)m * p.ldr + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * 64 + j * 32 + lr] = acc[i][j][v];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 4 + (lane >> 4);
+      const int m = m0 + wm * 32 * TM + i * 32 + row;
+      const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn);
+      if (m < p.M && nok) st4(p.C + (int64_t)m * p.ldc + n, x);
+    }
+  }
+}
+
 // XCD-contiguous tile ranges, group_m-grouped raster (m fastest inside a group).
-PIPNET_DEV void tile_coords(const GemmParams& p, int& m0, int& n0) {
+PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int nwg = p.mt * p.nt;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int gm = p.group_m;
@@ -125,11 +188,11 @@ PIPNET_DEV void tile_coords(const GemmParams& p, int& m0, int& n0) {
   const int first_m = group * gm;
   const int gsz = min(p.mt - first_m, gm);
   const int in_group = tile - group * gm * p.nt;
-  m0 = (first_m + in_group % gsz) * BM;
+  m0 = (first_m + in_group % gsz) * bm;
   n0 = (in_group / gsz) * BN;
 }
 
-PIPNET_DEV void zero_acc(f32x16 (&acc)[2][2]) {
+PIPNET_DEV void zero_acc(Acc& acc) {
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -141,12 +204,14 @@ PIPNET_DEV void zero_acc(f32x16 (&acc)[2][2]) {
 // ======================================================================================
 // main path: LDS-DMA staging, swizzled rows, pipelined fragments (K % BK == 0)
 // ======================================================================================
-template <int BK>
+template <int BK, int TM>
 struct Geo {
+  static constexpr int BMT = 64 * TM;                     // tile rows of A
   static constexpr int CHUNKS = BK / 4;                   // 16-B chunks per LDS row
   static constexpr int ROWS_PER_DMA = 64 / CHUNKS;        // rows one 1-KiB DMA fills
-  static constexpr int DMA_PER_WAVE = BM / ROWS_PER_DMA / NWAVES;
-  static constexpr int TILE_FLOATS = (BM + BN) * BK;      // one buffer: A rows then B rows
+  static constexpr int A_DMA = BMT / ROWS_PER_DMA / NWAVES;
+  static constexpr int B_DMA = BN / ROWS_PER_DMA / NWAVES;
+  static constexpr int TILE_FLOATS = (BMT + BN) * BK;     // one buffer: A rows then B rows
   static constexpr int NGROUPS = BK / 8;                  // 4-deep fragment groups per half-wave
   // chunk swizzle: the 16 lanes of a ds_read_b128 group read 16 distinct bank slots
   static PIPNET_DEV int swz(int row, int c) {
@@ -158,24 +223,28 @@ struct Frag {
   f32x4 a[2], b[2];
 };
 
-template <int BK>
+template <int BK, int TM>
 PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int lh, int q) {
-  using G = Geo<BK>;
+  using G = Geo<BK, TM>;
+  const int c = lh * (G::CHUNKS / 2) + q;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int ra = wm * 64 + i * 32 + lr;
-    const int rb = wn * 64 + i * 32 + lr;
-    const int c = lh * (G::CHUNKS / 2) + q;
+  for (int i = 0; i < TM; ++i) {
+    const int ra = wm * 32 * TM + i * 32 + lr;
     f.a[i] = ld4(buf + ra * BK + 4 * G::swz(ra, c));
-    f.b[i] = ld4(buf + BM * BK + rb * BK + 4 * G::swz(rb, c));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rb = wn * 64 + j * 32 + lr;
+    f.b[j] = ld4(buf + G::BMT * BK + rb * BK + 4 * G::swz(rb, c));
   }
 }
 
-PIPNET_DEV void mfma_frag(f32x16 (&acc)[2][2], const Frag& f) {
+template <int TM>
+PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
@@ -186,10 +255,23 @@ PIPNET_DEV void dma16(const float* src, float* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-template <int BK, int EPI, int ALOAD, int MINB>
+// Retire all but the NPEND youngest vector-memory ops of this wave (LDS-DMA counts as VMEM),
+// drain this wave's LDS reads, then the workgroup barrier -- one asm block, so hipcc cannot
+// widen it to vmcnt(0) (cdna_hip_programming.md 5, "Pipelining across barriers").
+template <int NPEND>
+PIPNET_DEV void wait_dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NPEND) : "memory");
+}
+
+// ABL (tuning-lab ablations only, 0 in the product): 1 = no DMA (stale LDS), 2 = no
+// epilogue (one store per lane keeps the accumulators live), 4 = no barrier.
+// NS = LDS stages: tile k+NS-1 is in flight while tile k is multiplied.
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
-  using G = Geo<BK>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * G::TILE_FLOATS];
+  using G = Geo<BK, TM>;
+  constexpr int DMA_PER_TILE = G::A_DMA + G::B_DMA;     // per wave
+  __shared__ __attribute__((aligned(16))) float smem[NS * G::TILE_FLOATS];
+  static_assert(NS * G::TILE_FLOATS >= 4 * 32 * 64, "vector epilogue needs 32 KiB of LDS");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -197,79 +279,117 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   const int wm = wid >> 1, wn = wid & 1;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, m0, n0);
+  tile_coords(p, G::BMT, m0, n0);
 
   // DMA sources: instruction i of this wave fills tile rows (i*NWAVES+wid)*ROWS_PER_DMA + ..;
   // lane writes row +lane/CHUNKS, physical chunk lane%CHUNKS -> fetches chunk c = swz(row, phys).
-  int64_t asrc[G::DMA_PER_WAVE];
-  const float* wsrc[G::DMA_PER_WAVE];
-  int achunk[G::DMA_PER_WAVE];
+  const int drow = lane / G::CHUNKS;
+  int64_t asrc[G::A_DMA];
+  int achunk[G::A_DMA];
+  const float* wsrc[G::B_DMA];
 #pragma unroll
-  for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
-    const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + lane / G::CHUNKS;
+  for (int i = 0; i < G::A_DMA; ++i) {
+    const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + drow;
     const int c = G::swz(row, lane % G::CHUNKS);
     achunk[i] = 4 * c;
-    const int m = min(m0 + row, p.M - 1);           // out-of-range rows: any valid row, never stored
-    const int n = min(n0 + row, p.N - 1);
-    asrc[i] = a_row_base<ALOAD>(p, m);
-    wsrc[i] = p.W + (int64_t)n * p.K + 4 * c;
+    asrc[i] = a_row_base<ALOAD>(p, min(m0 + row, p.M - 1));   // rows past M: valid, never stored
+  }
+#pragma unroll
+  for (int i = 0; i < G::B_DMA; ++i) {
+    const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + drow;
+    const int c = G::swz(row, lane % G::CHUNKS);
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 4 * c;
   }
   auto stage = [&](int kt, int buf) {
+    if (ABL & 1) return;
     float* base = smem + buf * G::TILE_FLOATS;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < G::DMA_PER_WAVE; ++i) {
-      const int rb = (i * NWAVES + wid) * G::ROWS_PER_DMA;
-      dma16(p.A + asrc[i] + a_col_off<ALOAD>(p, k0 + achunk[i]), base + rb * BK);
-      dma16(wsrc[i] + k0, base + BM * BK + rb * BK);
+    for (int i = 0; i < G::A_DMA; ++i)
+      dma16(p.A + asrc[i] + a_col_off<ALOAD>(p, k0 + achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+#pragma unroll
+    for (int i = 0; i < G::B_DMA; ++i)
+      dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+  };
+  // barrier once tile `need` has landed, `last` = youngest tile in flight
+  auto wait_tile = [&](int need, int last) {
+    if constexpr (NS == 2) {
+      __syncthreads();
+    } else {
+      const int pend = last - need;
+      if (NS >= 4 && pend >= 2) wait_dma_barrier<(NS >= 4 ? 2 : 0) * DMA_PER_TILE>();
+      else if (pend >= 1) wait_dma_barrier<DMA_PER_TILE>();
+      else wait_dma_barrier<0>();
     }
   };
 
-  f32x16 acc[2][2];
+  Acc acc;
   zero_acc(acc);
   const int nk = p.K / BK;
 
-  stage(0, 0);
-  __syncthreads();
+  int issued = -1;                                  // youngest tile whose DMA is in flight
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;
+  wait_tile(0, issued);
   Frag fa, fb;
-  read_frag<BK>(fa, smem, wm, wn, lr, lh, 0);
+  read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
     const float* buf = smem + cur * G::TILE_FLOATS;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    if constexpr (G::NGROUPS == 4) {
-      read_frag<BK>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag(acc, fa);
-      read_frag<BK>(fa, buf, wm, wn, lr, lh, 2);
-      mfma_frag(acc, fb);
-      read_frag<BK>(fb, buf, wm, wn, lr, lh, 3);
-      mfma_frag(acc, fa);
-    } else {
-      read_frag<BK>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag(acc, fa);
+    if (kt + NS - 1 < nk) {
+      int nb = cur + NS - 1;
+      if (nb >= NS) nb -= NS;
+      stage(kt + NS - 1, nb);
+      issued = kt + NS - 1;
     }
-    __syncthreads();                                  // tile kt+1 landed, tile kt fully read
-    if (kt + 1 < nk) read_frag<BK>(fa, smem + (cur ^ 1) * G::TILE_FLOATS, wm, wn, lr, lh, 0);
-    mfma_frag(acc, fb);
+    if constexpr (G::NGROUPS == 4) {
+      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+      mfma_frag<TM>(acc, fa);
+      read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
+      mfma_frag<TM>(acc, fb);
+      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
+      mfma_frag<TM>(acc, fa);
+    } else {
+      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+      mfma_frag<TM>(acc, fa);
+    }
+    const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
+    if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
+    if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
+    mfma_frag<TM>(acc, fb);
+    cur = nxt;
   }
-  epilogue<EPI>(p, acc, m0, n0, wm, wn, lr, lh);
+  if (ABL & 2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) t += acc[i][j][v];
+    p.C[(int64_t)blockIdx.x * NTHREADS + tid] = t;
+    return;
+  }
+  if (p.vec_epi)
+    epilogue_vec<EPI, TM>(p, acc, smem, m0, n0, wm, wn, lane, wid);
+  else
+    epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lr, lh);
 }
 
 // ======================================================================================
-// general path: register staging, zero-filled K tail (K % 4 == 0)
+// general path: register staging, zero-filled K tail (K % 4 == 0), 128x128x32 tiles
 // ======================================================================================
-constexpr int TBK = 32, LDK = TBK + 4;   // padded rows (144 B): conflict-free ds_read_b128
+constexpr int TBM = 128, TBK = 32, LDK = TBK + 4;   // padded rows (144 B): conflict-free ds_read_b128
 
 template <int EPI, int ALOAD>
 __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmParams p) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * (BM + BN) * LDK];
+  __shared__ __attribute__((aligned(16))) float smem[2 * (TBM + BN) * LDK];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, m0, n0);
+  tile_coords(p, TBM, m0, n0);
 
   const int srow = tid >> 3;
   const int sk = (tid & 7) * 4;
@@ -298,8 +418,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
     }
   };
   auto sstore = [&](int buf) {
-    float* As = smem + buf * (BM + BN) * LDK;
-    float* Bs = As + BM * LDK;
+    float* As = smem + buf * (TBM + BN) * LDK;
+    float* Bs = As + TBM * LDK;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       st4(As + (srow + 32 * i) * LDK + sk, ra[i]);
@@ -307,7 +427,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
     }
   };
 
-  f32x16 acc[2][2];
+  Acc acc;
   zero_acc(acc);
   const int nk = (p.K + TBK - 1) / TBK;
   gload(0);
@@ -316,8 +436,8 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const float* As = smem + buf * (BM + BN) * LDK;
-    const float* Bs = As + BM * LDK;
+    const float* As = smem + buf * (TBM + BN) * LDK;
+    const float* Bs = As + TBM * LDK;
     f32x4 fa[2][4], fb[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -340,7 +460,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
     if (kt + 1 < nk) sstore(buf ^ 1);
     __syncthreads();
   }
-  epilogue<EPI>(p, acc, m0, n0, wm, wn, lr, lh);
+  epilogue<EPI, 2>(p, acc, m0, n0, wm, wn, lr, lh);
 }
 
 }  // namespace pipnet_gemm

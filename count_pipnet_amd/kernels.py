@@ -32,14 +32,16 @@ def _launch(kname: str, flops: float, fn) -> None:
         _launch_hook(kname, flops, fn)
 
 
-def gemm_kernel_name(n: int, k: int, epilogue: int, aload: int) -> str:
-    """The rocprof name of the GEMM instantiation the library picks (mirrors launch_gemm in
+def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
+    """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant in
     csrc/gemm_f32.hip; alignment is always satisfied by torch allocations)."""
-    if k % 32 == 0 and k > 384 and n > 192:
-        return f"pipnet_gemm::gemm_f32_tn_kernel<32, {epilogue}, {aload}, 2>"
-    if k % 16 == 0:
-        return f"pipnet_gemm::gemm_f32_tn_kernel<16, {epilogue}, {aload}, 4>"
-    return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
+    if k % 16 == 0 and ((k <= 96 and n > 192 and m > 64) or (k % 32 and m > 64)):
+        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0>"
+    if k % 32:
+        return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
+    if n <= 384 or k <= 192 or m <= 64:
+        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0>"
+    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0>"
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
@@ -78,7 +80,7 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     if out is None:
         out = torch.empty((m, n), device=a.device, dtype=torch.float32)
     ldr = r.stride(0) if r is not None else 0
-    _launch(gemm_kernel_name(n, k, epilogue, 0), 2.0 * m * n * k,
+    _launch(gemm_kernel_name(m, n, k, epilogue, 0), 2.0 * m * n * k,
             lambda: _lib.call("pipnet_linear_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias), _ptr(scale),
                               _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue, _stream(a)))
     return out
@@ -91,7 +93,7 @@ def conv2x2(x_nhwc: Tensor, w_packed: Tensor, bias: Optional[Tensor], stride: in
     oh, ow = (h - 2) // stride + 1, (w - 2) // stride + 1
     y = torch.empty((b, oh, ow, cout), device=x_nhwc.device, dtype=torch.float32)
     epi = _lib.EPI_BIAS if bias is not None else _lib.EPI_NONE
-    _launch(gemm_kernel_name(cout, 4 * cin, epi, 1), 2.0 * b * oh * ow * cout * 4 * cin,
+    _launch(gemm_kernel_name(b * oh * ow, cout, 4 * cin, epi, 1), 2.0 * b * oh * ow * cout * 4 * cin,
             lambda: _lib.call("pipnet_conv2x2_f32", x_nhwc.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
                               cout, stride, y.data_ptr(), _stream(x_nhwc)))
     return y
