@@ -26,6 +26,9 @@ SIGNATURES = {
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_conv2x2_f32": [P, I32, I32, I32, I32, P, P, I32, I32, P, P],
     "pipnet_convnext_stem_f32": [P, I32, I32, I32, P, P, P, P, P, P],
+    "pipnet_conv2d_nhwc_f32": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, P],
+    "pipnet_maxpool2d_nhwc_f32": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
+    "pipnet_nchw_to_nhwc_f32": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_dwconv7_ln_f32": [P, I32, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_layernorm_f32": [P, I64, I32, P, P, P, P],
     "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],
@@ -36,7 +39,7 @@ SIGNATURES = {
 }
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p}
 
-EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL = 0, 1, 2, 3, 4
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
 
 _lib = None
 

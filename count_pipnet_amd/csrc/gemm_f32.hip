@@ -36,7 +36,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   p.vec_epi = (p.N % 4 == 0) && (p.ldc % 4 == 0) && aligned16(p.C) &&
               (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
               (!p.scale || aligned16(p.scale));
-  const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD == ALOAD_CONV2X2 || (p.lda & 3) == 0);
+  const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
   const int v = gemm_variant(p.M, p.N, p.K, vec);
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
@@ -53,6 +53,8 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
     PIPNET_EPI_CASE(PIPNET_EPI_BIAS_GELU)
     PIPNET_EPI_CASE(PIPNET_EPI_RESID)
     PIPNET_EPI_CASE(PIPNET_EPI_MUL)
+    PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RELU)
+    PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RESID_RELU)
     default: return PIPNET_ERR_ARG;
   }
 #undef PIPNET_EPI_CASE
@@ -67,10 +69,12 @@ extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, co
                                  int M, int N, int K, int epilogue, void* stream) {
   if (M < 0 || N < 0 || K <= 0) return PIPNET_ERR_ARG;
   if (M == 0 || N == 0) return PIPNET_OK;
-  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_MUL) return PIPNET_ERR_ARG;
+  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_BIAS_RESID_RELU) return PIPNET_ERR_ARG;
   if ((K & 3) || (lda & 3) || lda < K || ldc < N) return PIPNET_ERR_ARG;
   if (!A || !W || !C) return PIPNET_ERR_ARG;
-  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL) && (!R || ldr < N)) return PIPNET_ERR_ARG;
+  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU) &&
+      (!R || ldr < N))
+    return PIPNET_ERR_ARG;
   if (!aligned16(A) || !aligned16(W)) return PIPNET_ERR_ALIGN;
   GemmParams p{};
   p.A = A; p.lda = lda; p.W = W; p.bias = bias; p.scale = scale; p.R = R; p.ldr = ldr;
@@ -93,4 +97,30 @@ extern "C" int pipnet_conv2x2_f32(const float* x, int B, int H, int W, int Cin, 
   p.M = B * p.OH * p.OW; p.N = Cout; p.K = 4 * Cin;
   p.H = H; p.Wd = W; p.Cin = Cin; p.stride = stride;
   return launch_gemm<ALOAD_CONV2X2>(p, bias ? PIPNET_EPI_BIAS : PIPNET_EPI_NONE, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_conv2d_nhwc_f32(const float* x, int B, int H, int W, int Cin, const float* w_packed,
+                                      const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                      const float* R, int epilogue, float* y, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || (Cin & 3) || Cout <= 0 || KH <= 0 || KW <= 0 || stride <= 0 ||
+      pad < 0)
+    return PIPNET_ERR_ARG;
+  if (epilogue != PIPNET_EPI_NONE && epilogue != PIPNET_EPI_BIAS && epilogue != PIPNET_EPI_BIAS_RELU &&
+      epilogue != PIPNET_EPI_BIAS_RESID_RELU)
+    return PIPNET_ERR_ARG;
+  if (epilogue == PIPNET_EPI_BIAS_RESID_RELU && !R) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed)) return PIPNET_ERR_ALIGN;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  if (OH <= 0 || OW <= 0) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  GemmParams p{};
+  p.A = x; p.W = w_packed; p.bias = bias; p.R = R; p.ldr = Cout; p.C = y; p.ldc = Cout;
+  p.M = B * OH * OW; p.N = Cout; p.K = KH * KW * Cin;
+  p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
+    p.lda = Cin;
+    return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
+  }
+  return launch_gemm<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
 }

@@ -42,31 +42,59 @@ struct GemmParams {
   float* C;
   int64_t ldc;
   int M, N, K;
-  // implicit conv2x2 A-loader
-  int H, Wd, Cin, OH, OW, stride;
+  // implicit-GEMM convolution A-loaders (NHWC input [B][H][Wd][Cin])
+  int H, Wd, Cin, OH, OW, stride, KW, pad;
   int mt, nt, group_m;
   int vec_epi;     // 1: float4 epilogue through LDS (N, ldc, ldr % 4 == 0, C / R 16-B aligned)
 };
 
-enum { ALOAD_DENSE = 0, ALOAD_CONV2X2 = 1 };
+enum { ALOAD_DENSE = 0, ALOAD_CONV2X2 = 1, ALOAD_CONV = 2 };
+
+// 16 zero bytes: the LDS-DMA / float4 source for implicit-GEMM taps that fall in the
+// zero padding of a convolution (the DMA cannot zero-fill, but its source is per lane).
+static __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+
+// One A row (= one output pixel of a convolution, or one matrix row).
+struct ARow {
+  int64_t base;    // dense: m*lda; conv: offset of image b (and, for conv2x2, of the pixel)
+  int iy0, ix0;    // generic conv: top-left input coordinate of the receptive field
+};
 
 template <int ALOAD>
-PIPNET_DEV int64_t a_row_base(const GemmParams& p, int m) {
-  if (ALOAD == ALOAD_DENSE) return (int64_t)m * p.lda;
+PIPNET_DEV ARow a_row(const GemmParams& p, int m) {
+  ARow r{0, 0, 0};
+  if (ALOAD == ALOAD_DENSE) {
+    r.base = (int64_t)m * p.lda;
+    return r;
+  }
   const int ohw = p.OH * p.OW;
   const int b = m / ohw;
-  const int r = m - b * ohw;
-  const int oy = r / p.OW;
-  const int ox = r - oy * p.OW;
-  return (((int64_t)b * p.H + oy * p.stride) * p.Wd + ox * p.stride) * p.Cin;
+  const int rr = m - b * ohw;
+  const int oy = rr / p.OW;
+  const int ox = rr - oy * p.OW;
+  if (ALOAD == ALOAD_CONV2X2) {
+    r.base = (((int64_t)b * p.H + oy * p.stride) * p.Wd + ox * p.stride) * p.Cin;
+  } else {
+    r.base = (int64_t)b * p.H * p.Wd * p.Cin;
+    r.iy0 = oy * p.stride - p.pad;
+    r.ix0 = ox * p.stride - p.pad;
+  }
+  return r;
 }
 
+// Address of A[m][k .. k+3] (k % 4 == 0, the 4 channels of one tap), or of g_zero4.
 template <int ALOAD>
-PIPNET_DEV int64_t a_col_off(const GemmParams& p, int k) {
-  if (ALOAD == ALOAD_DENSE) return k;
-  const int idx = k / p.Cin;                 // (ky, kx) = (idx >> 1, idx & 1)
-  const int c = k - idx * p.Cin;
-  return ((int64_t)(idx >> 1) * p.Wd + (idx & 1)) * p.Cin + c;
+PIPNET_DEV const float* a_ptr(const GemmParams& p, const ARow& r, int k) {
+  if (ALOAD == ALOAD_DENSE) return p.A + r.base + k;
+  const int tap = k / p.Cin;
+  const int c = k - tap * p.Cin;
+  if (ALOAD == ALOAD_CONV2X2)          // (ky, kx) = (tap >> 1, tap & 1), never out of bounds
+    return p.A + r.base + ((int64_t)(tap >> 1) * p.Wd + (tap & 1)) * p.Cin + c;
+  const int ky = tap / p.KW;
+  const int iy = r.iy0 + ky;
+  const int ix = r.ix0 + tap - ky * p.KW;
+  if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero4;
+  return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + c;
 }
 
 // exact-enough GELU: x * Phi(x), Phi from erfc(|x|/sqrt2) by the Chebyshev fit of
@@ -99,8 +127,7 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
     const int n = n0 + wn * 64 + j * 32 + lr;
     if (n >= p.N) continue;
     float bn = 0.f, sn = 1.f;
-    if (EPI == PIPNET_EPI_BIAS || EPI == PIPNET_EPI_BIAS_GELU || EPI == PIPNET_EPI_RESID)
-      bn = p.bias ? p.bias[n] : 0.f;
+    if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL) bn = p.bias ? p.bias[n] : 0.f;
     if (EPI == PIPNET_EPI_RESID) sn = p.scale ? p.scale[n] : 1.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -113,6 +140,8 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
         if (EPI == PIPNET_EPI_BIAS_GELU) x = gelu_fast(x + bn);
         if (EPI == PIPNET_EPI_RESID) x = p.R[(int64_t)m * p.ldr + n] + sn * (x + bn);
         if (EPI == PIPNET_EPI_MUL) x = x * p.R[(int64_t)m * p.ldr + n];
+        if (EPI == PIPNET_EPI_BIAS_RELU) x = fmaxf(x + bn, 0.f);
+        if (EPI == PIPNET_EPI_BIAS_RESID_RELU) x = fmaxf(x + bn + p.R[(int64_t)m * p.ldr + n], 0.f);
         p.C[(int64_t)m * p.ldc + n] = x;
       }
     }
@@ -128,6 +157,16 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
   }
   if (EPI == PIPNET_EPI_RESID) x = r + sn * (x + bn);
   if (EPI == PIPNET_EPI_MUL) x = x * r;
+  if (EPI == PIPNET_EPI_BIAS_RELU) {
+    x = x + bn;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+  }
+  if (EPI == PIPNET_EPI_BIAS_RESID_RELU) {
+    x = x + bn + r;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = fmaxf(x[e], 0.f);
+  }
   return x;
 }
 
@@ -141,15 +180,14 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
 template <int EPI, int TM>
 PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, int m0, int n0, int wm, int wn,
                              int lane, int wid) {
-  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL;
+  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU;
   float* wt = smem + wid * 32 * 64;
   const int lr = lane & 31, lh = lane >> 5;
   const int c4 = lane & 15;
   const int n = n0 + wn * 64 + 4 * c4;
   const bool nok = n < p.N;
   f32x4 bn = {0.f, 0.f, 0.f, 0.f}, sn = {1.f, 1.f, 1.f, 1.f};
-  if ((EPI == PIPNET_EPI_BIAS || EPI == PIPNET_EPI_BIAS_GELU || EPI == PIPNET_EPI_RESID) && p.bias && nok)
-    bn = ld4(p.bias + n);
+  if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && p.bias && nok) bn = ld4(p.bias + n);
   if (EPI == PIPNET_EPI_RESID && p.scale && nok) sn = ld4(p.scale + n);
   f32x4 r[TM][8];
   if (HAS_R) {
@@ -284,7 +322,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   // DMA sources: instruction i of this wave fills tile rows (i*NWAVES+wid)*ROWS_PER_DMA + ..;
   // lane writes row +lane/CHUNKS, physical chunk lane%CHUNKS -> fetches chunk c = swz(row, phys).
   const int drow = lane / G::CHUNKS;
-  int64_t asrc[G::A_DMA];
+  ARow arow[G::A_DMA];
   int achunk[G::A_DMA];
   const float* wsrc[G::B_DMA];
 #pragma unroll
@@ -292,7 +330,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + drow;
     const int c = G::swz(row, lane % G::CHUNKS);
     achunk[i] = 4 * c;
-    asrc[i] = a_row_base<ALOAD>(p, min(m0 + row, p.M - 1));   // rows past M: valid, never stored
+    arow[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));   // rows past M: valid, never stored
   }
 #pragma unroll
   for (int i = 0; i < G::B_DMA; ++i) {
@@ -306,7 +344,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < G::A_DMA; ++i)
-      dma16(p.A + asrc[i] + a_col_off<ALOAD>(p, k0 + achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+      dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
 #pragma unroll
     for (int i = 0; i < G::B_DMA; ++i)
       dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
@@ -393,7 +431,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
 
   const int srow = tid >> 3;
   const int sk = (tid & 7) * 4;
-  int64_t abase[4];
+  ARow arow[4];
   bool aval[4];
   const float* wrow[4];
   bool wval[4];
@@ -401,7 +439,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
   for (int i = 0; i < 4; ++i) {
     const int m = m0 + srow + 32 * i;
     aval[i] = m < p.M;
-    abase[i] = a_row_base<ALOAD>(p, aval[i] ? m : 0);
+    arow[i] = a_row<ALOAD>(p, aval[i] ? m : 0);
     const int n = n0 + srow + 32 * i;
     wval[i] = n < p.N;
     wrow[i] = p.W + (int64_t)(wval[i] ? n : 0) * p.K;
@@ -410,10 +448,9 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
   auto gload = [&](int kt) {
     const int k = kt * TBK + sk;
     const bool kin = k < p.K;
-    const int64_t aoff = a_col_off<ALOAD>(p, kin ? k : 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      ra[i] = (aval[i] && kin) ? ld4(p.A + abase[i] + aoff) : f32x4{0.f, 0.f, 0.f, 0.f};
+      ra[i] = (aval[i] && kin) ? ld4(a_ptr<ALOAD>(p, arow[i], k)) : f32x4{0.f, 0.f, 0.f, 0.f};
       rb[i] = (wval[i] && kin) ? ld4(wrow[i] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };

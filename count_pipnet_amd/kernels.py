@@ -99,6 +99,42 @@ def conv2x2(x_nhwc: Tensor, w_packed: Tensor, bias: Optional[Tensor], stride: in
     return y
 
 
+def conv2d_nhwc(x: Tensor, w_packed: Tensor, bias: Optional[Tensor], stride: int, pad: int,
+                epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None) -> Tensor:
+    """NHWC implicit-GEMM convolution; w_packed [Cout, KH, KW, Cin]; r = residual (NHWC)."""
+    _chk(x, "conv input")
+    _chk(w_packed, "conv weight")
+    b, h, w, cin = x.shape
+    cout, kh, kw, wcin = w_packed.shape
+    if wcin != cin:
+        raise RuntimeError(f"conv2d_nhwc: input has {cin} channels, weight {wcin}")
+    oh, ow = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
+    y = torch.empty((b, oh, ow, cout), device=x.device, dtype=torch.float32)
+    m, k = b * oh * ow, kh * kw * cin
+    aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
+    _launch(gemm_kernel_name(m, cout, k, epilogue, aload), 2.0 * m * cout * k,
+            lambda: _lib.call("pipnet_conv2d_nhwc_f32", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
+                              cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), _stream(x)))
+    return y
+
+
+def maxpool2d_nhwc(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
+    _chk(x, "maxpool input")
+    b, h, w, c = x.shape
+    oh, ow = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    y = torch.empty((b, oh, ow, c), device=x.device, dtype=torch.float32)
+    _lib.call("pipnet_maxpool2d_nhwc_f32", x.data_ptr(), b, h, w, c, k, stride, pad, y.data_ptr(), _stream(x))
+    return y
+
+
+def nchw_to_nhwc(x: Tensor, cpad: int) -> Tensor:
+    _chk(x, "network input (NCHW)")
+    b, c, h, w = x.shape
+    y = torch.empty((b, h, w, cpad), device=x.device, dtype=torch.float32)
+    _lib.call("pipnet_nchw_to_nhwc_f32", x.data_ptr(), b, c, h, w, cpad, y.data_ptr(), _stream(x))
+    return y
+
+
 def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tensor) -> Tensor:
     _chk(x_nchw, "network input (NCHW)")
     n, c, h, wd = x_nchw.shape

@@ -1,12 +1,89 @@
-"""HIP executor for the ResNet feature backbones (resnet_features.py)."""
+"""HIP executor for the ResNet feature backbones (features/resnet_features.py:77-229).
+
+NHWC end to end.  Eval-mode BatchNorm is folded into each convolution at pack time
+(w' = w * g/sqrt(v+eps), b' = beta - mu * g/sqrt(v+eps)); every conv is one implicit-GEMM
+MFMA launch with bias / ReLU / identity-add+ReLU fused into its epilogue:
+
+  stem:        NCHW->NHWC (channels padded 3->4) -> conv7x7 s2 p3 +BN+ReLU -> maxpool 3x3 s2 p1
+  Bottleneck:  conv1x1+BN+ReLU -> conv3x3(s)+BN+ReLU -> conv1x1+BN (+ downsample conv1x1(s)+BN)
+               + identity -> ReLU  (the last three in one epilogue)
+  BasicBlock:  conv3x3(s)+BN+ReLU -> conv3x3+BN + identity -> ReLU
+
+Folded weights are cached per device and rebuilt whenever any of the conv / BN tensors
+changes (storage pointer or in-place version counter).
+"""
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, Optional
 
 import torch
+import torch.nn as nn
+
+from . import _lib
+from . import kernels as K
+
+Tensor = torch.Tensor
 
 
-def resnet_features_hip(model, x: torch.Tensor, cache: Dict) -> torch.Tensor:
-    raise NotImplementedError(
-        "count_pipnet_amd: the ResNet HIP path is not built yet; run ResNet backbones on the "
-        "torch path explicitly with `with count_pipnet_amd.backend.torch_backend(): ...`")
+def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Optional[int] = None):
+    ts = [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    if conv.bias is not None:
+        ts.append(conv.bias)
+    stamp = tuple((t.data_ptr(), t._version) for t in ts) + (bn.eps,)
+    ck = (key, str(conv.weight.device))
+    ent = cache.get(ck)
+    if ent is None or ent[0] != stamp:
+        with torch.no_grad():
+            scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+            w = conv.weight * scale.view(-1, 1, 1, 1)
+            b = bn.bias - bn.running_mean * scale
+            if conv.bias is not None:
+                b = b + conv.bias * scale
+            w = w.permute(0, 2, 3, 1)                           # [Cout, KH, KW, Cin]
+            if cpad is not None and cpad > w.shape[3]:
+                w = torch.nn.functional.pad(w, (0, cpad - w.shape[3]))
+            ent = (stamp, (w.contiguous().float(), b.contiguous().float()))
+        cache[ck] = ent
+    return ent[1]
+
+
+def _conv_bn(cache, key, conv, bn, x, epilogue, r=None, cpad=None):
+    if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
+        raise RuntimeError(f"ResNet HIP path: unsupported conv {conv}")
+    w, b = _fold(cache, key, conv, bn, cpad)
+    return K.conv2d_nhwc(x, w, b, conv.stride[0], conv.padding[0], epilogue, r)
+
+
+def _bottleneck(cache, key, blk, h):
+    from .resnet_features import BasicBlock, Bottleneck
+    if blk.downsample is not None:
+        ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
+        idt = _conv_bn(cache, key + ".ds", ds_conv, ds_bn, h, _lib.EPI_BIAS)
+    else:
+        idt = h
+    if isinstance(blk, Bottleneck):
+        t = _conv_bn(cache, key + ".c1", blk.conv1, blk.bn1, h, _lib.EPI_BIAS_RELU)
+        t = _conv_bn(cache, key + ".c2", blk.conv2, blk.bn2, t, _lib.EPI_BIAS_RELU)
+        return _conv_bn(cache, key + ".c3", blk.conv3, blk.bn3, t, _lib.EPI_BIAS_RESID_RELU, r=idt)
+    if isinstance(blk, BasicBlock):
+        t = _conv_bn(cache, key + ".c1", blk.conv1, blk.bn1, h, _lib.EPI_BIAS_RELU)
+        return _conv_bn(cache, key + ".c2", blk.conv2, blk.bn2, t, _lib.EPI_BIAS_RESID_RELU, r=idt)
+    raise RuntimeError(f"ResNet HIP path: unsupported block {type(blk).__name__}")
+
+
+def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
+    """ResNet_features.forward (resnet_features.py:211-222) on HIP kernels -> NHWC features."""
+    K.require_device(x, "network input")
+    x = x.contiguous()
+    if x.shape[1] != 3:
+        raise RuntimeError(f"ResNet stem expects 3 input channels, got {x.shape[1]}")
+    mp = model.maxpool
+    if not (mp.kernel_size == 3 and mp.stride == 2 and mp.padding == 1):
+        raise RuntimeError(f"ResNet HIP path: unsupported stem pool {mp}")
+    h = K.nchw_to_nhwc(x, 4)
+    h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=4)
+    h = K.maxpool2d_nhwc(h, 3, 2, 1)
+    for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4)):
+        for j, blk in enumerate(layer):
+            h = _bottleneck(cache, f"layer{li + 1}.{j}", blk, h)
+    return h

@@ -36,6 +36,8 @@ extern "C" {
 #define PIPNET_EPI_BIAS_GELU 2  /* C = gelu_erf(A W^T + b)          (CNBlock Linear1+GELU) */
 #define PIPNET_EPI_RESID 3      /* C = R + s * (A W^T + b)   (CNBlock Linear2*layer_scale+x)*/
 #define PIPNET_EPI_MUL 4        /* C = (A W^T) * R          (BilinearIntermediate W(e)*V(e)) */
+#define PIPNET_EPI_BIAS_RELU 5  /* C = relu(A W^T + b)            (ResNet conv+BN+ReLU)      */
+#define PIPNET_EPI_BIAS_RESID_RELU 6 /* C = relu(A W^T + b + R) (Bottleneck conv3+BN+identity+ReLU) */
 
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -58,6 +60,24 @@ int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* 
  * features/convnext_features.py:5-15.  Cin % 32 == 0. */
 int pipnet_conv2x2_f32(const float* x, int B, int H, int W, int Cin, const float* w_packed,
                        const float* bias, int Cout, int stride, float* y, void* stream);
+
+/* General NHWC convolution as implicit GEMM on MFMA (ResNet backbones, eval BatchNorm
+ * folded into w/bias by the caller):  y = epi(conv(x, w) + bias), epilogue one of
+ * PIPNET_EPI_NONE / _BIAS / _BIAS_RELU / _BIAS_RESID_RELU (R: [B,OH,OW,Cout]).
+ * x: [B,H,W,Cin] NHWC, w_packed: [Cout][KH][KW][Cin], y: [B,OH,OW,Cout] with
+ * OH = (H + 2 pad - KH)/stride + 1.  Replaces the Conv2d+BatchNorm2d(+ReLU)(+identity)
+ * sequences of features/resnet_features.py:77-124,126-229.  Cin % 4 == 0. */
+int pipnet_conv2d_nhwc_f32(const float* x, int B, int H, int W, int Cin, const float* w_packed,
+                           const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                           const float* R, int epilogue, float* y, void* stream);
+
+/* MaxPool2d(k, stride, pad) on NHWC (ResNet stem, resnet_features.py:136). */
+int pipnet_maxpool2d_nhwc_f32(const float* x, int B, int H, int W, int C, int k, int stride, int pad,
+                              float* y, void* stream);
+
+/* NCHW -> NHWC with the channel dimension zero-padded to Cpad (network input of the ResNet
+ * stem, so every implicit-GEMM tap is a 16-byte vector). */
+int pipnet_nchw_to_nhwc_f32(const float* x, int B, int C, int H, int W, int Cpad, float* y, void* stream);
 
 /* ConvNeXt stem: Conv2d(3,96,k4,s4,bias) + LayerNorm2d(96, eps 1e-6)  (features.0).
  * x: [B,3,H,W] NCHW (the reference's own input layout), w: [96,3,4,4] as torch stores it,

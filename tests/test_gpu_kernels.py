@@ -189,3 +189,39 @@ def test_count_finish_and_encode(gpu):
     w = torch.tensor([1 / 3, 2 / 3, 1.0], device=gpu)
     lin = K.count_encode(x, 3, kind=1, do_round=False, w=w).cpu()
     assert torch.allclose(lin, (x.cpu().reshape(-1, 1) * w.cpu()).view(4, 9))
+
+
+@pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
+    (64, 64, 56, 3, 1, 1, _lib.EPI_BIAS_RELU), (128, 128, 56, 3, 2, 1, _lib.EPI_BIAS_RELU),
+    (256, 1024, 28, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU), (64, 256, 56, 1, 1, 0, _lib.EPI_BIAS),
+    (256, 512, 56, 1, 2, 0, _lib.EPI_BIAS), (4, 64, 64, 7, 2, 3, _lib.EPI_BIAS_RELU),
+    (12, 40, 9, 3, 1, 1, _lib.EPI_NONE), (32, 48, 7, 5, 2, 2, _lib.EPI_BIAS_RESID_RELU)])
+def test_conv2d_nhwc(gpu, cin, cout, h, k, s, pad, epi):
+    g = torch.Generator().manual_seed(cin * 7 + h + k)
+    x = _rand(2, cin, h, h, gen=g)
+    w = _rand(cout, cin, k, k, gen=g, scale=1.0 / (cin * k * k) ** 0.5)
+    b = _rand(cout, gen=g)
+    y = F.conv2d(x, w, b if epi != _lib.EPI_NONE else None, stride=s, padding=pad)
+    r = _rand(*y.shape, gen=g)
+    if epi == _lib.EPI_BIAS_RELU:
+        y = torch.relu(y)
+    if epi == _lib.EPI_BIAS_RESID_RELU:
+        y = torch.relu(y + r)
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    out = K.conv2d_nhwc(d(x.permute(0, 2, 3, 1).contiguous()), d(w.permute(0, 2, 3, 1).contiguous()),
+                        d(b) if epi != _lib.EPI_NONE else None, s, pad, epi,
+                        d(r.permute(0, 2, 3, 1).contiguous()) if epi == _lib.EPI_BIAS_RESID_RELU else None)
+    ref = y.permute(0, 2, 3, 1)
+    assert torch.allclose(out.double().cpu(), ref, rtol=2e-5, atol=2e-5), (out.double().cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("c,h", [(64, 112), (8, 9)])
+def test_maxpool_and_relayout(gpu, c, h):
+    g = torch.Generator().manual_seed(c + h)
+    x = torch.randn(2, c, h, h, generator=g)
+    ref = F.max_pool2d(x, 3, 2, 1).permute(0, 2, 3, 1)
+    out = K.maxpool2d_nhwc(x.permute(0, 2, 3, 1).contiguous().to(gpu), 3, 2, 1).cpu()
+    assert torch.equal(out, ref)
+    xin = torch.randn(2, 3, h, h, generator=g)
+    y = K.nchw_to_nhwc(xin.to(gpu), 4).cpu()
+    assert torch.equal(y[..., :3], xin.permute(0, 2, 3, 1)) and torch.all(y[..., 3] == 0)

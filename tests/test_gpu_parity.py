@@ -19,7 +19,7 @@ from oracle import ref_cpu
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-3
-HIP_CASES = [n for n in golden_names() if load_golden(n)[0]["case"]["net"] != "resnet50"]
+HIP_CASES = golden_names()
 
 
 def _check_pipnet(proto, pooled, out, r_pooled, r_out, r_proto_max, r_proto_sum, inference):
