@@ -100,28 +100,20 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     a = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
     from count_pipnet_amd import build, kernels
+    from count_pipnet_amd.dist import ShardedInference, init_from_env
+    rank, world, dev = init_from_env()
     build.build()
     from count_pipnet_amd.synthetic import synth_images
     net, _ = make_net(dev)
+    # one process per GPU, weights resident, this rank's 64-image shard already in HBM; the
+    # step ends with the RCCL all-gather of pooled + logits (DataParallel's gather)
+    sharded = ShardedInference(net)
     xs = synth_images(a.batch, 224, seed=100 + rank).to(dev)
-    gather_out = [torch.empty(a.batch, 200, device=dev) for _ in range(world)]
-    gather_pooled = [torch.empty(a.batch, 768, device=dev) for _ in range(world)]
 
     def step():
         with torch.no_grad():
-            _, pooled, out = net(xs, inference=True)
-            if world > 1:
-                dist.all_gather(gather_out, out)
-                dist.all_gather(gather_pooled, pooled)
+            _, pooled, out = sharded(xs, inference=True, global_batch=False, sizes=[a.batch] * world)
         return out
 
     def barrier():

@@ -1,0 +1,71 @@
+"""Multi-process data-parallel inference (count_pipnet_amd.dist) on CPU with gloo,
+world_size 2: DataParallel-style sharding (torch.chunk order, uneven shards) and the
+all-gather of pooled / logits reproduce the single-process full-batch forward."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from count_pipnet_amd.dist import ShardedInference, shard_sizes
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, batch, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+        from count_pipnet_amd.backend import torch_backend
+        from golden_util import golden_inputs, load_golden
+        from model_util import build_model
+        meta, _ = load_golden("pipnet_mid_addon")
+        net = build_model(meta)
+        xs = torch.cat([golden_inputs(meta)] * 2)[:batch]
+        wrapped = ShardedInference(net)
+        with torch.no_grad(), torch_backend():
+            proto, pooled, out = wrapped(xs, inference=True)
+            _, r_pooled, r_out = net(xs, inference=True)
+            start = sum(shard_sizes(batch, world)[:rank])
+            own = shard_sizes(batch, world)[rank]
+            # per-rank shard path: each rank passes only its own rows
+            _, pooled2, out2 = wrapped(xs[start:start + own], inference=True, global_batch=False)
+        ok = (torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5)
+              and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto.shape[0] == own
+              and wrapped.module is net)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("batch", [4, 5])
+def test_sharded_inference_gloo_world2(batch):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, batch, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    res = dict(q.get(timeout=5) for _ in range(2))
+    assert res == {0: True, 1: True}
+
+
+def test_shard_sizes_match_torch_chunk():
+    for b in range(0, 20):
+        for w in (1, 2, 3, 4, 8):
+            ref = [c.shape[0] for c in torch.arange(b).chunk(w)] if b else []
+            ref += [0] * (w - len(ref))
+            assert shard_sizes(b, w) == ref, (b, w)
