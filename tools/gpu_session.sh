@@ -20,6 +20,7 @@ for s in $STEPS; do
     gemm)  timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemm_bench.log 2>&1; stop_if_fatal $? gemm; grep -v "^\[" gpurun_out/gemm_bench.log | tail -20 ;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; stop_if_fatal $? bench; tail -3 gpurun_out/bench.log ;;
     prof)  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1); stop_if_fatal $? prof; find gpurun_out/prof -name "*stats*" | head ;;
+    pmc)   timeout -k 10 900 bash tools/pmc.sh > gpurun_out/pmc.log 2>&1; stop_if_fatal $? pmc; tail -25 gpurun_out/pmc.log ;;
   esac
 done
 exit 0

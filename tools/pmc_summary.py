@@ -20,8 +20,9 @@ def load(pass_dir):
 
 
 def short(name):
-    m = re.search(r"(\w+)(<[^>]*>)?\(", name)
-    return (m.group(1) + (m.group(2) or "")) if m else name[:60]
+    m = re.search(r"((?:\w+::)*\w+)(<[^>]*>)?\(", name)
+    k = (m.group(1) + (m.group(2) or "")) if m else name[:60]
+    return k.replace("(anonymous namespace)::", "")
 
 
 agg = defaultdict(lambda: defaultdict(list))
@@ -50,3 +51,14 @@ for k, c in sorted(agg.items(), key=lambda kv: -sum(kv[1].get("dur_ns_p1", [0]))
     out[k] = dict(launches=n, avg_us=dur / 1e3, clock_ghz=clk, mfma_busy=mfu, sq_busy=busy,
                   hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes=rd + wr)
 json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+# the dominant MFMA kernel (largest total time) -> bench.py roofline.traffic
+gemms = {k: v for k, v in out.items() if "gemm_f32_tn" in k}
+if gemms:
+    dom = max(gemms, key=lambda k: gemms[k]["avg_us"] * gemms[k]["launches"])
+    tr = dict(kernel_key=dom, hbm_bytes_per_launch=gemms[dom]["hbm_bytes"],
+              hbm_read_bytes_per_launch=gemms[dom]["hbm_read_bytes"],
+              hbm_write_bytes_per_launch=gemms[dom]["hbm_write_bytes"], avg_us=gemms[dom]["avg_us"],
+              method="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh); "
+                     "FETCH_SIZE x2 (gfx950 wide-read undercount), KB -> bytes")
+    json.dump(tr, open(os.path.join(d, "traffic_latest.json"), "w"), indent=1)
+    print("dominant:", json.dumps(tr))
