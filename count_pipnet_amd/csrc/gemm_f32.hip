@@ -29,6 +29,25 @@ int gemm_variant(int M, int N, int K, bool vec) {
   return 3;
 }
 
+// split-K reduction + epilogue: C = epi(sum_s slab_s), float4 per thread.
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restrict__ ws, int splits, int64_t slab,
+                                                            int M, int N, const float* __restrict__ bias,
+                                                            const float* __restrict__ scale, const float* R,
+                                                            int64_t ldr, float* C, int64_t ldc) {
+  const int n4 = N / 4;
+  const int64_t total = (int64_t)M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / n4), n = 4 * (int)(i - (int64_t)m * n4);
+    f32x4 acc = ld4(ws + (int64_t)m * N + n);
+    for (int sp = 1; sp < splits; ++sp) acc += ld4(ws + sp * slab + (int64_t)m * N + n);
+    const f32x4 bn = bias ? ld4(bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 sn = scale ? ld4(scale + n) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const f32x4 r = R ? ld4(R + (int64_t)m * ldr + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    st4(C + (int64_t)m * ldc + n, epi_math<EPI>(acc, bn, sn, r));
+  }
+}
+
 template <int ALOAD>
 int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   p.nt = (p.N + BN - 1) / BN;
@@ -123,4 +142,54 @@ extern "C" int pipnet_conv2d_nhwc_f32(const float* x, int B, int H, int W, int C
     return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
   }
   return launch_gemm<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float* W, const float* bias,
+                                        const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
+                                        int M, int N, int K, int epilogue, int splits, float* workspace,
+                                        void* stream) {
+  if (splits <= 1) return pipnet_linear_f32(A, lda, W, bias, scale, R, ldr, C, ldc, M, N, K, epilogue, stream);
+  if (M < 0 || N <= 0 || K <= 0 || (N & 3) || (K % 32) || (lda & 3) || lda < K || (ldc & 3) || ldc < N)
+    return PIPNET_ERR_ARG;
+  if (splits > K / 32 || splits > 64 || !workspace || !A || !W || !C) return PIPNET_ERR_ARG;
+  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_BIAS_RESID_RELU)
+    return PIPNET_ERR_ARG;
+  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU) &&
+      (!R || ldr < N || (ldr & 3) || !aligned16(R)))
+    return PIPNET_ERR_ARG;
+  if (!aligned16(A) || !aligned16(W) || !aligned16(C) || !aligned16(workspace) || (bias && !aligned16(bias)) ||
+      (scale && !aligned16(scale)))
+    return PIPNET_ERR_ALIGN;
+  if (M == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  GemmParams p{};
+  p.A = A; p.lda = lda; p.W = W; p.C = workspace; p.ldc = N; p.M = M; p.N = N; p.K = K;
+  p.nt = (N + BN - 1) / BN;
+  p.mt = (M + 63) / 64;
+  p.group_m = choose_group_m(p);
+  p.vec_epi = 1;
+  p.split_stride = (int64_t)M * N;
+  const dim3 grid(p.mt * p.nt, splits);
+  hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, PIPNET_EPI_NONE, ALOAD_DENSE, 3, 2>), grid, dim3(NTHREADS), 0, s, p);
+  PIPNET_CHECK_LAUNCH();
+  const int64_t work = (int64_t)M * (N / 4);
+  const int blocks = (int)((work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096);
+#define PIPNET_RED(E)                                                                                           \
+  case E:                                                                                                      \
+    hipLaunchKernelGGL((splitk_reduce_kernel<E>), dim3(blocks), dim3(256), 0, s, workspace, splits, p.split_stride, \
+                       M, N, bias, scale, R, ldr, C, ldc);                                                     \
+    break;
+  switch (epilogue) {
+    PIPNET_RED(PIPNET_EPI_NONE)
+    PIPNET_RED(PIPNET_EPI_BIAS)
+    PIPNET_RED(PIPNET_EPI_BIAS_GELU)
+    PIPNET_RED(PIPNET_EPI_RESID)
+    PIPNET_RED(PIPNET_EPI_MUL)
+    PIPNET_RED(PIPNET_EPI_BIAS_RELU)
+    PIPNET_RED(PIPNET_EPI_BIAS_RESID_RELU)
+    default: return PIPNET_ERR_ARG;
+  }
+#undef PIPNET_RED
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
 }

@@ -46,6 +46,9 @@ struct GemmParams {
   int H, Wd, Cin, OH, OW, stride, KW, pad;
   int mt, nt, group_m;
   int vec_epi;     // 1: float4 epilogue through LDS (N, ldc, ldr % 4 == 0, C / R 16-B aligned)
+  int stagger;     // lab: workgroups [stagger_lo, stagger_hi) sleep stagger x s_sleep(127) first
+  int stagger_lo, stagger_hi;
+  int64_t split_stride;   // split-K (gridDim.y > 1): slab y of C starts at C + y * split_stride
 };
 
 enum { ALOAD_DENSE = 0, ALOAD_CONV2X2 = 1, ALOAD_CONV = 2 };
@@ -307,6 +310,11 @@ PIPNET_DEV void wait_dma_barrier() {
 template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
   using G = Geo<BK, TM>;
+  // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
+  const int nk_all = p.K / BK;
+  const int kt_begin = (int)((int64_t)nk_all * blockIdx.y / gridDim.y);
+  const int nk = (int)((int64_t)nk_all * (blockIdx.y + 1) / gridDim.y) - kt_begin;
+  p.C += (int64_t)blockIdx.y * p.split_stride;
   constexpr int DMA_PER_TILE = G::A_DMA + G::B_DMA;     // per wave
   __shared__ __attribute__((aligned(16))) float smem[NS * G::TILE_FLOATS];
   static_assert(NS * G::TILE_FLOATS >= 4 * 32 * 64, "vector epilogue needs 32 KiB of LDS");
@@ -318,6 +326,8 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
   tile_coords(p, G::BMT, m0, n0);
+  if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi)
+    for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
   // DMA sources: instruction i of this wave fills tile rows (i*NWAVES+wid)*ROWS_PER_DMA + ..;
   // lane writes row +lane/CHUNKS, physical chunk lane%CHUNKS -> fetches chunk c = swz(row, phys).
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   auto stage = [&](int kt, int buf) {
     if (ABL & 1) return;
     float* base = smem + buf * G::TILE_FLOATS;
-    const int k0 = kt * BK;
+    const int k0 = (kt_begin + kt) * BK;
 #pragma unroll
     for (int i = 0; i < G::A_DMA; ++i)
       dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
@@ -363,7 +373,6 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
 
   Acc acc;
   zero_acc(acc);
-  const int nk = p.K / BK;
 
   int issued = -1;                                  // youngest tile whose DMA is in flight
   for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;

@@ -44,6 +44,17 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0>"
 
 
+def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
+    """K slabs for short-M GEMMs: enough workgroups to cover every CU at least once, each
+    slab >= 8 K-tiles of 32 (the Bilinear intermediate at M = batch has only 48 tiles)."""
+    if n % 4 or k % 32:
+        return 1
+    tiles = -(-m // 64) * -(-n // 128)
+    if tiles >= cus:
+        return 1
+    return max(1, min(-(-cus // tiles), k // 256, 64))
+
+
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -80,6 +91,14 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     if out is None:
         out = torch.empty((m, n), device=a.device, dtype=torch.float32)
     ldr = r.stride(0) if r is not None else 0
+    splits = splitk_factor(m, n, k)
+    if splits > 1:
+        ws = torch.empty((splits, m, n), device=a.device, dtype=torch.float32)
+        _launch(f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, 0, 0, 3, 2, 0>", 2.0 * m * n * k,
+                lambda: _lib.call("pipnet_linear_splitk_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias),
+                                  _ptr(scale), _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue, splits,
+                                  ws.data_ptr(), _stream(a)))
+        return out
     _launch(gemm_kernel_name(m, n, k, epilogue, 0), 2.0 * m * n * k,
             lambda: _lib.call("pipnet_linear_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias), _ptr(scale),
                               _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue, _stream(a)))

@@ -53,6 +53,16 @@ int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* 
                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                       int M, int N, int K, int epilogue, void* stream);
 
+/* Split-K variant for short-M products (M <= a few hundred rows, long K: the Bilinear /
+ * LinearFull intermediate GEMMs at M = batch, count_pipnet_utils.py:342-385): the K range
+ * is cut into `splits` slabs computed by separate workgroups into `workspace`
+ * (splits * M * N floats), then one reduction kernel sums the slabs and applies the
+ * epilogue.  N % 4 == 0, K % 32 == 0, splits <= K/32. */
+int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float* W, const float* bias,
+                             const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
+                             int M, int N, int K, int epilogue, int splits, float* workspace,
+                             void* stream);
+
 /* ConvNeXt downsample conv, k=2, stride s in {1,2}, no padding, as implicit GEMM on MFMA.
  * x: [B,H,W,Cin] NHWC (already LayerNorm2d-normalised), w_packed: [Cout][2][2][Cin]
  * (torch weight [Cout,Cin,2,2] permuted), y: [B,OH,OW,Cout], OH=(H-2)/s+1.

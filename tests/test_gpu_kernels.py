@@ -225,3 +225,21 @@ def test_maxpool_and_relayout(gpu, c, h):
     xin = torch.randn(2, 3, h, h, generator=g)
     y = K.nchw_to_nhwc(xin.to(gpu), 4).cpu()
     assert torch.equal(y[..., :3], xin.permute(0, 2, 3, 1)) and torch.all(y[..., 3] == 0)
+
+
+@pytest.mark.parametrize("epi", [_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_MUL, _lib.EPI_RESID, _lib.EPI_BIAS_GELU])
+def test_linear_splitk(gpu, epi):
+    """Short-M products take the split-K path (workspace slabs + reducing epilogue)."""
+    from count_pipnet_amd.kernels import splitk_factor
+    g = torch.Generator().manual_seed(100 + epi)
+    m, n, k = 37, 1536, 2048
+    assert splitk_factor(m, n, k) > 1
+    a, w, b = _rand(m, k, gen=g), _rand(n, k, gen=g, scale=0.03), _rand(n, gen=g)
+    s, r = _rand(n, gen=g), _rand(m, n, gen=g)
+    acc = a @ w.t()
+    ref = {_lib.EPI_NONE: acc, _lib.EPI_BIAS: acc + b, _lib.EPI_MUL: acc * r, _lib.EPI_RESID: r + s * (acc + b),
+           _lib.EPI_BIAS_GELU: F.gelu(acc + b)}[epi]
+    d = lambda t: t.float().to(gpu)  # noqa: E731
+    out = K.linear(d(a), d(w), d(b), epi, scale=d(s), r=d(r)).double().cpu()
+    tol = 4e-6 * (1 + ref.abs()) + 4e-6 * ((a.abs() @ w.abs().t()) * (1 + s.abs() + r.abs()))
+    assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()

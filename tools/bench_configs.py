@@ -1,0 +1,86 @@
+"""Throughput of the non-headline BASELINE configs on one GPU (bench.py measures configs[1]).
+
+  C1  CountPIPNet identity.yaml, 64x64, bs=16          (the reference's CPU case; here on HIP)
+  C3  PIP-Net ResNet50 224x224, bs=128, fp32           (BASELINE names bf16; fp32 here = exact)
+  C5  CountPIPNet bilinear 2048 prototypes, 128x128, 64 images per GPU (bs=256 over 4 GPUs)
+  C2' PIP-Net ConvNeXt-tiny-13 224x224, bs=64          (the 13x13 variant)
+
+    python tools/bench_configs.py [--steps 10] [--only c5]
+Prints one JSON line per config (images/sec, ms/step, model TFLOP/s where defined).
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from count_pipnet_amd import build  # noqa: E402
+from count_pipnet_amd.count_pipnet import get_count_network  # noqa: E402
+from count_pipnet_amd.pipnet import get_pipnet  # noqa: E402
+from count_pipnet_amd.synthetic import fill_module_, synth_images  # noqa: E402
+
+CONFIGS = {
+    "c1": dict(model="count", batch=16, size=64, classes=9,
+               args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=16,
+                         activation="gumbel_softmax", intermediate_layer="identity", max_count=3, use_ste=True,
+                         bias=False), gflop=0.2495),
+    "c3": dict(model="pipnet", batch=128, size=224, classes=200, args=dict(net="resnet50", num_features=0, bias=False),
+               gflop=38.16),
+    "c5": dict(model="count", batch=64, size=128, classes=9,
+               args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=2048,
+                         activation="gumbel_softmax", intermediate_layer="bilinear", max_count=3, use_ste=True,
+                         bias=False), gflop=1.374),
+    "c2_13": dict(model="pipnet", batch=64, size=224, classes=200,
+                  args=dict(net="convnext_tiny_13", num_features=0, bias=False), gflop=12.617),
+}
+
+
+def make(cfg, dev):
+    a = argparse.Namespace(disable_pretrained=True, backward_clamp_strategy="Gated", **cfg["args"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        if cfg["model"] == "pipnet":
+            net, _ = get_pipnet(cfg["classes"], a)
+        else:
+            net, _ = get_count_network(cfg["classes"], a, max_count=a.max_count, use_ste=a.use_ste)
+    fill_module_(net, 7, "trained")
+    return net.eval().to(dev)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    build.build()
+    dev = torch.device("cuda:0")
+    for name, cfg in CONFIGS.items():
+        if a.only and name != a.only:
+            continue
+        net = make(cfg, dev)
+        xs = synth_images(cfg["batch"], cfg["size"], seed=5).to(dev)
+        with torch.no_grad():
+            for _ in range(a.warmup):
+                net(xs, inference=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                net(xs, inference=True)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+        ips = cfg["batch"] * a.steps / el
+        print(json.dumps(dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
+                              image_size=cfg["size"], dtype="f32",
+                              model_tflops=ips * cfg["gflop"] / 1e3,
+                              model_frac_of_f32_peak=ips * cfg["gflop"] / 1e3 / 157.3)), flush=True)
+        del net, xs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

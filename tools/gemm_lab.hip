@@ -26,6 +26,11 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
   p.group_m = group_m;
   p.vec_epi = variant >= 20 ? 0 : 1;
   if (variant >= 20) variant -= 20;
+  // group_m >= 100: stagger experiment, group_m = 100*s + g
+  p.stagger = group_m / 100;
+  p.group_m = group_m % 100;
+  p.stagger_lo = 256;
+  p.stagger_hi = 512;
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
     case 0: launch<32, 2, 2, 2>(p, epi, s); break;
