@@ -1,0 +1,158 @@
+// bf16 ResNet path (BASELINE C3): implicit-GEMM convolution (gemm_bf16_impl.hpp), NCHW fp32
+// -> NHWC bf16 input relayout, NHWC bf16 max-pool.  Reference: features/resnet_features.py
+// (conv / BatchNorm / ReLU / Bottleneck / MaxPool2d, :77-229).
+#include "gemm_bf16_impl.hpp"
+
+using namespace pipnet_bf16;
+
+namespace {
+
+int grid_for(int64_t n) { return (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192); }
+
+int choose_group_m(int K) {
+  const double panel = 128.0 * K * 2.0;
+  int g = (int)(2.0 * 1024 * 1024 / panel);
+  return g < 1 ? 1 : (g > 16 ? 16 : g);
+}
+
+template <int ALOAD>
+int launch_conv(ConvParams& p, int epi, hipStream_t s) {
+  p.nt = (p.N + BN - 1) / BN;
+  p.group_m = choose_group_m(p.K);
+  // 128-row tiles unless that leaves fewer than two workgroups per CU
+  const bool tm2 = (int64_t)((p.M + 127) / 128) * p.nt >= 512;
+  p.mt = tm2 ? (p.M + 127) / 128 : (p.M + 63) / 64;
+  const dim3 grid(p.mt * p.nt), block(NTHREADS);
+#define PIPNET_BF_CASE(E)                                                                        \
+  case E:                                                                                       \
+    if (tm2) hipLaunchKernelGGL((conv_bf16_kernel<2, E, ALOAD, 2>), grid, block, 0, s, p);      \
+    else hipLaunchKernelGGL((conv_bf16_kernel<1, E, ALOAD, 3>), grid, block, 0, s, p);          \
+    break;
+  switch (epi) {
+    PIPNET_BF_CASE(PIPNET_EPI_NONE)
+    PIPNET_BF_CASE(PIPNET_EPI_BIAS)
+    PIPNET_BF_CASE(PIPNET_EPI_BIAS_RELU)
+    PIPNET_BF_CASE(PIPNET_EPI_BIAS_RESID_RELU)
+    default: return PIPNET_ERR_ARG;
+  }
+#undef PIPNET_BF_CASE
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+// [B,C,H,W] fp32 -> [B,H,W,Cpad] bf16 (RNE, channels >= C zero); Cpad % 8 == 0, one
+// thread per pixel writes one or more 16-B chunks.
+__global__ __launch_bounds__(256) void nchw_to_nhwc_bf16_kernel(const float* __restrict__ x, int B, int C, int H,
+                                                                int W, int Cpad, bf16* __restrict__ y) {
+  const int64_t hw = (int64_t)H * W;
+  const int64_t n = (int64_t)B * hw;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / hw;
+    const int64_t pix = i - b * hw;
+    for (int c0 = 0; c0 < Cpad; c0 += 8) {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)(c0 + e < C ? x[(b * C + c0 + e) * hw + pix] : 0.f);
+      *reinterpret_cast<bf16x8*>(y + i * Cpad + c0) = o;
+    }
+  }
+}
+
+// MaxPool2d on NHWC bf16, 8 channels (16 B) per thread; max is exact in bf16 and padding
+// never wins (torch pads max-pool with -inf).
+__global__ __launch_bounds__(256) void maxpool_nhwc_bf16_kernel(const bf16* __restrict__ x, int B, int H, int W,
+                                                                int C, int k, int stride, int pad, int OH, int OW,
+                                                                bf16* __restrict__ y) {
+  const int QC = C / 8;
+  const int64_t n = (int64_t)B * OH * OW * QC;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int q = (int)(i % QC);
+    const int64_t pix = i / QC;
+    const int ox = (int)(pix % OW);
+    const int oy = (int)((pix / OW) % OH);
+    const int64_t b = pix / ((int64_t)OW * OH);
+    float m[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m[e] = -INFINITY;
+    for (int ky = 0; ky < k; ++ky) {
+      const int iy = oy * stride - pad + ky;
+      if (iy < 0 || iy >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int ix = ox * stride - pad + kx;
+        if (ix < 0 || ix >= W) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + (((b * H + iy) * W + ix) * C) + 8 * q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m[e] = fmaxf(m[e], (float)v[e]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)m[e];   // exact: every m[e] is a bf16 value
+    *reinterpret_cast<bf16x8*>(y + pix * C + 8 * q) = o;
+  }
+}
+
+}  // namespace
+
+extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                                       const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                       const void* R, int epilogue, void* y, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || (Cin & 7) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
+      stride <= 0 || pad < 0)
+    return PIPNET_ERR_ARG;
+  if (epilogue != PIPNET_EPI_NONE && epilogue != PIPNET_EPI_BIAS && epilogue != PIPNET_EPI_BIAS_RELU &&
+      epilogue != PIPNET_EPI_BIAS_RESID_RELU)
+    return PIPNET_ERR_ARG;
+  if (epilogue == PIPNET_EPI_BIAS_RESID_RELU && !R) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y) || (R && !aligned16(R)) || (bias && !aligned16(bias)))
+    return PIPNET_ERR_ALIGN;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  if (OH <= 0 || OW <= 0) return PIPNET_ERR_ARG;
+  if ((int64_t)B * OH * OW >= (int64_t)1 << 31) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  ConvParams p{};
+  p.A = reinterpret_cast<const bf16*>(x);
+  p.W = reinterpret_cast<const bf16*>(w_packed);
+  p.bias = bias;
+  p.R = reinterpret_cast<const bf16*>(R);
+  p.ldr = Cout;
+  p.C = reinterpret_cast<bf16*>(y);
+  p.ldc = Cout;
+  p.M = B * OH * OW; p.N = Cout;
+  p.Kv = KH * KW * Cin;
+  p.K = (p.Kv + BK - 1) / BK * BK;
+  p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
+    p.lda = Cin;
+    return launch_conv<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
+  }
+  return launch_conv<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y,
+                                        void* stream) {
+  if (B < 0 || C <= 0 || H <= 0 || W <= 0 || Cpad < C || (Cpad & 7) || !x || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(y)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel, dim3(grid_for((int64_t)B * H * W)), dim3(256), 0,
+                     (hipStream_t)stream, x, B, C, H, W, Cpad, reinterpret_cast<bf16*>(y));
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k, int stride, int pad,
+                                          void* y, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || C <= 0 || (C & 7) || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)
+    return PIPNET_ERR_ARG;
+  if (!x || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(y)) return PIPNET_ERR_ALIGN;
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  if (OH <= 0 || OW <= 0) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(maxpool_nhwc_bf16_kernel, dim3(grid_for((int64_t)B * OH * OW * (C / 8))), dim3(256), 0,
+                     (hipStream_t)stream, reinterpret_cast<const bf16*>(x), B, H, W, C, k, stride, pad, OH, OW,
+                     reinterpret_cast<bf16*>(y));
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}

@@ -1,0 +1,290 @@
+// bf16 implicit-GEMM convolution on gfx950 matrix cores (v_mfma_f32_32x32x16_bf16), fp32
+// accumulation, bf16 NHWC activations in and out.  Serves the ResNet backbones in the
+// BASELINE C3 configuration ("PIP-Net ResNet50 ... bf16 inference"; SURVEY.md 8a a7:
+// "FP32 ref; build bf16"): every conv + folded BatchNorm (+ReLU, + identity-add+ReLU) of
+// features/resnet_features.py:77-229 is one launch of this kernel.
+//
+// Same "TN" product and tile machinery as the fp32 kernel (gemm_f32_impl.hpp), byte for
+// byte: an LDS row is 128 B (BK = 64 bf16 = 8 16-B chunks, chunk index XOR-swizzled by
+// (row>>1)&7 at the DMA source, undone on the read), global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, 16 B = 8 channels per lane).  For 32x32x16 bf16 lane l supplies
+// A[l&31][k = 8(l>>5) + j] and B[k][l&31], j = 0..7 -- one ds_read_b128 per operand; the
+// k order inside a tile is free, so half-wave h reads chunks 4h .. 4h+3 (one MFMA k-step
+// per chunk pair), exactly the fp32 kernel's access pattern.
+//
+// K is padded to a multiple of 64 at pack time (zero weight rows); the A loader returns
+// the zero chunk for k >= Kv (the valid K) and for taps in the convolution's padding, so
+// one kernel covers the 7x7x8 stem (K 392 -> 448) as well as 1x1 and 3x3 convs.
+// Requires Cin % 8 == 0 (a 16-B chunk never straddles two taps).
+#pragma once
+#include "common.hpp"
+
+namespace pipnet_bf16 {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64, BN = 128, NTHREADS = 256, NWAVES = 4;
+constexpr int CHUNKS = 8, ROWS_PER_DMA = 8;   // 128-B rows; one 1-KiB DMA fills 8 rows
+
+struct ConvParams {
+  const bf16* A;
+  int64_t lda;         // dense rows (1x1 stride-1 convs): row pitch in elements
+  const bf16* W;       // [N][K] (K padded to 64, zero beyond Kv)
+  const float* bias;   // [N] fp32 (folded BatchNorm shift), may be null
+  const bf16* R;       // residual [M][ldr] bf16 (EPI_BIAS_RESID_RELU)
+  int64_t ldr;
+  bf16* C;
+  int64_t ldc;
+  int M, N, K, Kv;
+  int H, Wd, Cin, OH, OW, stride, KW, pad;
+  int mt, nt, group_m;
+};
+
+enum { ALOAD_DENSE = 0, ALOAD_CONV = 2 };
+
+static __device__ __attribute__((aligned(16))) float g_zero_bf[4] = {0.f, 0.f, 0.f, 0.f};
+
+struct ARow {
+  int64_t base;
+  int iy0, ix0;
+};
+
+template <int ALOAD>
+PIPNET_DEV ARow a_row(const ConvParams& p, int m) {
+  ARow r{0, 0, 0};
+  if (ALOAD == ALOAD_DENSE) {
+    r.base = (int64_t)m * p.lda;
+    return r;
+  }
+  const int ohw = p.OH * p.OW;
+  const int b = m / ohw;
+  const int rr = m - b * ohw;
+  const int oy = rr / p.OW;
+  const int ox = rr - oy * p.OW;
+  r.base = (int64_t)b * p.H * p.Wd * p.Cin;
+  r.iy0 = oy * p.stride - p.pad;
+  r.ix0 = ox * p.stride - p.pad;
+  return r;
+}
+
+// Address of A[m][k .. k+7] (8 channels of one tap), or of the zero chunk.
+template <int ALOAD>
+PIPNET_DEV const void* a_ptr(const ConvParams& p, const ARow& r, int k) {
+  if (k >= p.Kv) return g_zero_bf;
+  if (ALOAD == ALOAD_DENSE) return p.A + r.base + k;
+  const int tap = k / p.Cin;
+  const int c = k - tap * p.Cin;
+  const int ky = tap / p.KW;
+  const int iy = r.iy0 + ky;
+  const int ix = r.ix0 + tap - ky * p.KW;
+  if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
+  return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + c;
+}
+
+PIPNET_DEV int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
+
+template <int TM>
+struct Geo {
+  static constexpr int BMT = 64 * TM;
+  static constexpr int A_DMA = BMT / ROWS_PER_DMA / NWAVES;
+  static constexpr int B_DMA = BN / ROWS_PER_DMA / NWAVES;
+  static constexpr int TILE_ELEMS = (BMT + BN) * BK;   // bf16 elements of one stage
+};
+
+template <int TM>
+struct Frag {
+  bf16x8 a[TM], b[2];
+};
+template <int TM>
+using Acc = f32x16[TM][2];
+
+template <int TM>
+PIPNET_DEV void read_frag(Frag<TM>& f, const bf16* buf, int wm, int wn, int lr, int lh, int q) {
+  const int c = lh * 4 + q;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ra = wm * 32 * TM + i * 32 + lr;
+    f.a[i] = *reinterpret_cast<const bf16x8*>(buf + ra * BK + 8 * swz(ra, c));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int rb = wn * 64 + j * 32 + lr;
+    f.b[j] = *reinterpret_cast<const bf16x8*>(buf + Geo<TM>::BMT * BK + rb * BK + 8 * swz(rb, c));
+  }
+}
+
+template <int TM>
+PIPNET_DEV void mfma_frag(Acc<TM>& acc, const Frag<TM>& f) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+}
+
+PIPNET_DEV void dma16(const void* src, bf16* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int& m0, int& n0) {
+  const int nwg = p.mt * p.nt;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int gm = p.group_m;
+  const int group = tile / (gm * p.nt);
+  const int first_m = group * gm;
+  const int gsz = min(p.mt - first_m, gm);
+  const int in_group = tile - group * gm * p.nt;
+  m0 = (first_m + in_group % gsz) * bm;
+  n0 = (in_group / gsz) * BN;
+}
+
+PIPNET_DEV u32x4 as_u32x4(const bf16x8& v) { return __builtin_bit_cast(u32x4, v); }
+
+// Epilogue: each wave re-lays its 32x64 fp32 accumulator slice through LDS (rows padded to
+// 68 floats: the 16-B reads of 8 consecutive lanes then cover all 64 banks), then every
+// lane finishes 8 consecutive channels of one pixel -- bias, residual (one 16-B bf16
+// load, all issued before the first store), ReLU, round-to-nearest-even to bf16
+// (v_cvt_pk_bf16_f32), one 16-B store.  Needs N % 8 == 0 and 16-B aligned C / R rows.
+constexpr int EPI_LD = 68;
+
+template <int EPI, int TM>
+PIPNET_DEV void epilogue(const ConvParams& p, const Acc<TM>& acc, float* smem, int m0, int n0, int wm, int wn,
+                         int lane, int wid) {
+  constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
+  float* wt = smem + wid * 32 * EPI_LD;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int c8 = lane & 7;
+  const int n = n0 + wn * 64 + 8 * c8;
+  const bool nok = n < p.N;
+  f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
+    b0 = ld4(p.bias + n);
+    b1 = ld4(p.bias + n + 4);
+  }
+  bf16x8 r[TM][4];
+  if (HAS_R) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int m = min(m0 + wm * 32 * TM + i * 32 + it * 8 + (lane >> 3), p.M - 1);
+        if (nok) r[i][it] = *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + n);
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * EPI_LD + j * 32 + lr] = acc[i][j][v];
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const int m = m0 + wm * 32 * TM + i * 32 + row;
+      f32x4 x0 = ld4(wt + row * EPI_LD + 8 * c8), x1 = ld4(wt + row * EPI_LD + 8 * c8 + 4);
+      x0 += b0;
+      x1 += b1;
+      if (HAS_R) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] += (float)r[i][it][e];
+          x1[e] += (float)r[i][it][4 + e];
+        }
+      }
+      if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] = fmaxf(x0[e], 0.f);
+          x1[e] = fmaxf(x1[e], 0.f);
+        }
+      }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (bf16)x0[e];
+        o[4 + e] = (bf16)x1[e];
+      }
+      if (m < p.M && nok) *reinterpret_cast<bf16x8*>(p.C + (int64_t)m * p.ldc + n) = o;
+    }
+  }
+}
+
+// TM = 1: 64x128 tiles, TM = 2: 128x128; 4 waves in 2x2, 2 LDS stages, one barrier per
+// 64-deep K tile, fragments software-pipelined over the tile's 4 chunk groups.
+template <int TM, int EPI, int ALOAD, int MINB>
+__global__ __launch_bounds__(NTHREADS, MINB) void conv_bf16_kernel(ConvParams p) {
+  using G = Geo<TM>;
+  constexpr int NS = 2;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * G::TILE_ELEMS];
+  static_assert(NS * G::TILE_ELEMS * 2 >= NWAVES * 32 * EPI_LD * 4, "epilogue LDS");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  int m0, n0;
+  tile_coords(p, G::BMT, m0, n0);
+  const int nk = p.K / BK;
+
+  const int drow = lane / CHUNKS;
+  ARow arow[G::A_DMA];
+  int achunk[G::A_DMA];
+  const bf16* wsrc[G::B_DMA];
+#pragma unroll
+  for (int i = 0; i < G::A_DMA; ++i) {
+    const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
+    achunk[i] = 8 * swz(row, lane % CHUNKS);
+    arow[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
+  }
+#pragma unroll
+  for (int i = 0; i < G::B_DMA; ++i) {
+    const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * swz(row, lane % CHUNKS);
+  }
+  auto stage = [&](int kt, int buf) {
+    bf16* base = smem + buf * G::TILE_ELEMS;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < G::A_DMA; ++i)
+      dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
+#pragma unroll
+    for (int i = 0; i < G::B_DMA; ++i)
+      dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
+  };
+
+  Acc<TM> acc;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+
+  stage(0, 0);
+  __syncthreads();
+  Frag<TM> fa, fb;
+  read_frag<TM>(fa, smem, wm, wn, lr, lh, 0);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bf16* buf = smem + cur * G::TILE_ELEMS;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    read_frag<TM>(fb, buf, wm, wn, lr, lh, 1);
+    mfma_frag<TM>(acc, fa);
+    read_frag<TM>(fa, buf, wm, wn, lr, lh, 2);
+    mfma_frag<TM>(acc, fb);
+    read_frag<TM>(fb, buf, wm, wn, lr, lh, 3);
+    mfma_frag<TM>(acc, fa);
+    __syncthreads();                                     // tile kt+1 landed, tile kt read
+    if (kt + 1 < nk) read_frag<TM>(fa, smem + (cur ^ 1) * G::TILE_ELEMS, wm, wn, lr, lh, 0);
+    mfma_frag<TM>(acc, fb);
+    cur ^= 1;
+  }
+  epilogue<EPI, TM>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
+}
+
+}  // namespace pipnet_bf16

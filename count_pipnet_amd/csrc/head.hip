@@ -15,8 +15,8 @@ constexpr int HEAD_THREADS = 256;
 constexpr int PIX_PER_BLOCK = 32;
 
 // ---------------------------------------------------------------------------------------
-template <int NJ, int MODE>   // MODE 0 = max pool, 1 = sum pool
-__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const float* __restrict__ feat, int HW, int P,
+template <int NJ, int MODE, typename T = float>   // MODE 0 = max pool, 1 = sum pool; T = float / __bf16 logits
+__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __restrict__ feat, int HW, int P,
                                                                     float* __restrict__ proto,
                                                                     float* __restrict__ pooled) {
   __shared__ float red[HEAD_THREADS / 64][NJ * 64];
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const float*
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
-      v[j] = c < P ? feat[base + c] : -INFINITY;
+      v[j] = c < P ? (float)feat[base + c] : -INFINITY;
       m = fmaxf(m, v[j]);
     }
     m = wave_max(m);
@@ -255,8 +255,9 @@ int nj_bucket(int P) {
     default: return PIPNET_ERR_ARG; \
   }
 
-extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
-                                       float* pooled, void* stream) {
+template <typename T>
+int softmax_pool_launch(const T* feat, int B, int HW, int P, int pool_mode, float* proto, float* pooled,
+                        void* stream) {
   if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1)) return PIPNET_ERR_ARG;
   if (!feat || !proto || !pooled) return PIPNET_ERR_ARG;
   if (B == 0) return PIPNET_OK;
@@ -265,15 +266,25 @@ extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, 
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(pooled, 0, sizeof(float) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
-#define SP_CALL(N)                                                                                       \
-  if (pool_mode == 0)                                                                                    \
-    hipLaunchKernelGGL((softmax_pool_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled); \
-  else                                                                                                   \
-    hipLaunchKernelGGL((softmax_pool_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled);
+#define SP_CALL(N)                                                                                          \
+  if (pool_mode == 0)                                                                                       \
+    hipLaunchKernelGGL((softmax_pool_kernel<N, 0, T>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled); \
+  else                                                                                                      \
+    hipLaunchKernelGGL((softmax_pool_kernel<N, 1, T>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled);
   PIPNET_NJ_SWITCH(nj, SP_CALL)
 #undef SP_CALL
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
+}
+
+extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
+                                       float* pooled, void* stream) {
+  return softmax_pool_launch(feat, B, HW, P, pool_mode, proto, pooled, stream);
+}
+
+extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
+                                        float* pooled, void* stream) {
+  return softmax_pool_launch(reinterpret_cast<const __bf16*>(feat), B, HW, P, pool_mode, proto, pooled, stream);
 }
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,

@@ -154,6 +154,88 @@ def nchw_to_nhwc(x: Tensor, cpad: int) -> Tensor:
     return y
 
 
+# ---- bf16 ResNet path (BASELINE C3) ---------------------------------------------------
+
+BF16_KTILE = 64
+
+
+def _chk_bf(t: Tensor, what: str) -> None:
+    if not (t.is_cuda and t.dtype == torch.bfloat16):
+        raise RuntimeError(f"count_pipnet_amd: {what} must be a bfloat16 ROCm device tensor "
+                           f"(got device={t.device}, dtype={t.dtype}); there is no CPU fallback")
+    if not t.is_contiguous():
+        raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
+
+
+def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int) -> str:
+    """rocprof name of the bf16 conv instantiation (mirrors launch_conv in csrc/conv_bf16.hip)."""
+    tm2 = -(-m // 128) * -(-n // 128) >= 512
+    return (f"pipnet_bf16::conv_bf16_kernel<2, {epilogue}, {aload}, 2>" if tm2
+            else f"pipnet_bf16::conv_bf16_kernel<1, {epilogue}, {aload}, 3>")
+
+
+def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
+    """[Cout, KH, KW, Cin] (fp32) -> [Cout, Kp] bf16, Kp = KH*KW*Cin rounded up to 64 (zeros)."""
+    cout = w_ohwi.shape[0]
+    k = w_ohwi[0].numel()
+    kp = -(-k // BF16_KTILE) * BF16_KTILE
+    out = torch.zeros((cout, kp), device=w_ohwi.device, dtype=torch.bfloat16)
+    out[:, :k] = w_ohwi.reshape(cout, k).to(torch.bfloat16)
+    return out
+
+
+def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Optional[Tensor], stride: int,
+                     pad: int, epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None) -> Tensor:
+    """NHWC bf16 implicit-GEMM convolution; w_packed from pack_conv_weight_bf16; bias fp32."""
+    _chk_bf(x, "conv input")
+    _chk_bf(w_packed, "conv weight")
+    if r is not None:
+        _chk_bf(r, "residual")
+    if bias is not None:
+        _chk(bias, "conv bias")
+    b, h, w, cin = x.shape
+    cout, kp = w_packed.shape
+    k = kh * kw * cin
+    if kp != -(-k // BF16_KTILE) * BF16_KTILE:
+        raise RuntimeError(f"conv2d_nhwc_bf16: packed weight K {kp} does not match {kh}x{kw}x{cin}")
+    oh, ow = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
+    y = torch.empty((b, oh, ow, cout), device=x.device, dtype=torch.bfloat16)
+    m = b * oh * ow
+    aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload), 2.0 * m * cout * k,
+            lambda: _lib.call("pipnet_conv2d_nhwc_bf16", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
+                              _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), _stream(x)))
+    return y
+
+
+def maxpool2d_nhwc_bf16(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
+    _chk_bf(x, "maxpool input")
+    b, h, w, c = x.shape
+    oh, ow = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    y = torch.empty((b, oh, ow, c), device=x.device, dtype=torch.bfloat16)
+    _lib.call("pipnet_maxpool2d_nhwc_bf16", x.data_ptr(), b, h, w, c, k, stride, pad, y.data_ptr(), _stream(x))
+    return y
+
+
+def nchw_to_nhwc_bf16(x: Tensor, cpad: int) -> Tensor:
+    _chk(x, "network input (NCHW)")
+    b, c, h, w = x.shape
+    y = torch.empty((b, h, w, cpad), device=x.device, dtype=torch.bfloat16)
+    _lib.call("pipnet_nchw_to_nhwc_bf16", x.data_ptr(), b, c, h, w, cpad, y.data_ptr(), _stream(x))
+    return y
+
+
+def softmax_pool_bf16(feat_nhwc: Tensor, pool_mode: int) -> Tuple[Tensor, Tensor]:
+    """bf16 logits [B,h,w,P] -> fp32 (proto [B,h,w,P], pooled [B,P])."""
+    _chk_bf(feat_nhwc, "prototype logits")
+    b, h, w, p = feat_nhwc.shape
+    proto = torch.empty((b, h, w, p), device=feat_nhwc.device, dtype=torch.float32)
+    pooled = torch.empty((b, p), device=feat_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_softmax_pool_bf16", feat_nhwc.data_ptr(), b, h * w, p, pool_mode, proto.data_ptr(),
+              pooled.data_ptr(), _stream(feat_nhwc))
+    return proto, pooled
+
+
 def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tensor) -> Tensor:
     _chk(x_nchw, "network input (NCHW)")
     n, c, h, wd = x_nchw.shape

@@ -62,7 +62,10 @@ class PIPNet(nn.Module):
         logits = add_on_logits_hip(self._add_on, feats)    # [B,h,w,P]
         if not (isinstance(self._pool, nn.Sequential) and isinstance(self._pool[0], nn.AdaptiveMaxPool2d)):
             raise RuntimeError("PIPNet HIP path expects _pool = Sequential(AdaptiveMaxPool2d(1), Flatten())")
-        proto, pooled = K.softmax_pool(logits, pool_mode=0)
+        if logits.dtype == torch.bfloat16:
+            proto, pooled = K.softmax_pool_bf16(logits, pool_mode=0)
+        else:
+            proto, pooled = K.softmax_pool(logits, pool_mode=0)
         cls = self._classification
         clamped, out = K.nonneg_linear(pooled, cls.weight, cls.bias, PRESENCE_THRESHOLD if inference else None)
         return nhwc_as_nchw(proto), (clamped if inference else pooled), out
@@ -82,6 +85,13 @@ def add_on_logits_hip(add_on: nn.Module, feats: Tensor, activation=nn.Softmax) -
         raise RuntimeError(f"HIP head expects _add_on = [Conv2d 1x1, activation], got {add_on}")
     b, h, w, c = feats.shape
     p = conv.out_channels
+    if feats.dtype == torch.bfloat16:                    # bf16 build: 1x1 conv on bf16 MFMA
+        from .convnext_features import packed
+        cache = add_on.__dict__.setdefault("_hip_pack", {})
+        wb = packed(cache, "add_on_bf16", conv.weight,
+                    lambda t: K.pack_conv_weight_bf16(t.detach().view(p, 1, 1, c).float()))
+        bias = conv.bias.detach().float().contiguous() if conv.bias is not None else None
+        return K.conv2d_nhwc_bf16(feats, wb, 1, 1, bias, 1, 0, _lib.EPI_BIAS if bias is not None else _lib.EPI_NONE)
     y = K.linear(feats.view(-1, c), conv.weight.view(p, c), conv.bias,
                  _lib.EPI_BIAS if conv.bias is not None else _lib.EPI_NONE)
     return y.view(b, h, w, p)
@@ -146,9 +156,30 @@ def get_pip_network(num_classes: int, args: argparse.Namespace):
     return backbone, add_on, pool, classification, num_prototypes
 
 
+def set_hip_dtype(model: nn.Module, dtype) -> nn.Module:
+    """Select the compute dtype of the HIP inference path: torch.float32 (default, exact
+    parity with the reference) or torch.bfloat16 (the BASELINE C3 ResNet build).  bf16 is
+    implemented for the ResNet backbones only."""
+    from .resnet_features import ResNet_features
+    dtype = {"fp32": torch.float32, "f32": torch.float32, "bf16": torch.bfloat16}.get(dtype, dtype)
+    if dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"unsupported HIP compute dtype {dtype}")
+    found = False
+    for m in model.modules():
+        if isinstance(m, ResNet_features):
+            m.hip_dtype = dtype
+            found = True
+    if dtype == torch.bfloat16 and not found:
+        raise ValueError("the bf16 HIP path is implemented for ResNet backbones only")
+    return model
+
+
 def get_pipnet(num_classes: int, args: argparse.Namespace):
-    """pipnet.py:117-139 -> (PIPNet, num_prototypes)."""
+    """pipnet.py:117-139 -> (PIPNet, num_prototypes).  Optional ``args.hip_dtype``
+    ("fp32" | "bf16") selects the HIP compute dtype (see set_hip_dtype)."""
     feature_net, add_on, pool, classification, num_prototypes = get_pip_network(num_classes, args)
     model = PIPNet(num_classes=num_classes, num_prototypes=num_prototypes, feature_net=feature_net, args=args,
                    add_on_layers=add_on, pool_layer=pool, classification_layer=classification)
+    if getattr(args, "hip_dtype", None):
+        set_hip_dtype(model, args.hip_dtype)
     return model, num_prototypes

@@ -110,6 +110,9 @@ class ResNet_features(nn.Module):
                 elif isinstance(m, BasicBlock):
                     nn.init.constant_(m.bn2.weight, 0)
         self._hip_pack: Dict = {}
+        # compute dtype of the HIP inference path: torch.float32 (exact, the reference's) or
+        # torch.bfloat16 (BASELINE C3 build; features come back as bf16 NHWC-backed views)
+        self.hip_dtype = torch.float32
 
     def _make_layer(self, block, planes, num_blocks, stride=1):
         downsample = None

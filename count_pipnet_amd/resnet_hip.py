@@ -11,6 +11,11 @@ MFMA launch with bias / ReLU / identity-add+ReLU fused into its epilogue:
 
 Folded weights are cached per device and rebuilt whenever any of the conv / BN tensors
 changes (storage pointer or in-place version counter).
+
+``model.hip_dtype = torch.bfloat16`` selects the bf16 build (BASELINE C3): activations bf16
+NHWC, folded weights rounded to bf16 once at pack time ([Cout][KH*KW*Cin padded to 64]),
+biases fp32, fp32 accumulation on v_mfma_f32_32x32x16_bf16, every conv output rounded to
+nearest even.  The stem input is padded 3 -> 8 channels (one 16-B chunk per tap).
 """
 from __future__ import annotations
 
@@ -25,12 +30,13 @@ from . import kernels as K
 Tensor = torch.Tensor
 
 
-def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Optional[int] = None):
+def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Optional[int] = None,
+          bf16: bool = False):
     ts = [conv.weight, bn.weight, bn.bias, bn.running_mean, bn.running_var]
     if conv.bias is not None:
         ts.append(conv.bias)
     stamp = tuple((t.data_ptr(), t._version) for t in ts) + (bn.eps,)
-    ck = (key, str(conv.weight.device))
+    ck = (key, str(conv.weight.device), bf16)
     ent = cache.get(ck)
     if ent is None or ent[0] != stamp:
         with torch.no_grad():
@@ -42,7 +48,10 @@ def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Opti
             w = w.permute(0, 2, 3, 1)                           # [Cout, KH, KW, Cin]
             if cpad is not None and cpad > w.shape[3]:
                 w = torch.nn.functional.pad(w, (0, cpad - w.shape[3]))
-            ent = (stamp, (w.contiguous().float(), b.contiguous().float()))
+            w = w.contiguous().float()
+            if bf16:
+                w = K.pack_conv_weight_bf16(w)
+            ent = (stamp, (w, b.contiguous().float()))
         cache[ck] = ent
     return ent[1]
 
@@ -50,6 +59,10 @@ def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Opti
 def _conv_bn(cache, key, conv, bn, x, epilogue, r=None, cpad=None):
     if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
         raise RuntimeError(f"ResNet HIP path: unsupported conv {conv}")
+    if x.dtype == torch.bfloat16:
+        w, b = _fold(cache, key, conv, bn, cpad, bf16=True)
+        kh, kw = conv.kernel_size
+        return K.conv2d_nhwc_bf16(x, w, kh, kw, b, conv.stride[0], conv.padding[0], epilogue, r)
     w, b = _fold(cache, key, conv, bn, cpad)
     return K.conv2d_nhwc(x, w, b, conv.stride[0], conv.padding[0], epilogue, r)
 
@@ -72,7 +85,8 @@ def _bottleneck(cache, key, blk, h):
 
 
 def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
-    """ResNet_features.forward (resnet_features.py:211-222) on HIP kernels -> NHWC features."""
+    """ResNet_features.forward (resnet_features.py:211-222) on HIP kernels -> NHWC features
+    (fp32, or bf16 when ``model.hip_dtype`` is torch.bfloat16)."""
     K.require_device(x, "network input")
     x = x.contiguous()
     if x.shape[1] != 3:
@@ -80,9 +94,14 @@ def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
     mp = model.maxpool
     if not (mp.kernel_size == 3 and mp.stride == 2 and mp.padding == 1):
         raise RuntimeError(f"ResNet HIP path: unsupported stem pool {mp}")
-    h = K.nchw_to_nhwc(x, 4)
-    h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=4)
-    h = K.maxpool2d_nhwc(h, 3, 2, 1)
+    if getattr(model, "hip_dtype", torch.float32) == torch.bfloat16:
+        h = K.nchw_to_nhwc_bf16(x, 8)
+        h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=8)
+        h = K.maxpool2d_nhwc_bf16(h, 3, 2, 1)
+    else:
+        h = K.nchw_to_nhwc(x, 4)
+        h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=4)
+        h = K.maxpool2d_nhwc(h, 3, 2, 1)
     for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4)):
         for j, blk in enumerate(layer):
             h = _bottleneck(cache, f"layer{li + 1}.{j}", blk, h)

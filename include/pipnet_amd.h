@@ -89,6 +89,27 @@ int pipnet_maxpool2d_nhwc_f32(const float* x, int B, int H, int W, int C, int k,
  * stem, so every implicit-GEMM tap is a 16-byte vector). */
 int pipnet_nchw_to_nhwc_f32(const float* x, int B, int C, int H, int W, int Cpad, float* y, void* stream);
 
+/* ---- bf16 ResNet path (BASELINE C3 "ResNet50 ... bf16 inference") -------------------
+ * Activations are bf16 NHWC (passed as void*: raw 16-bit bfloat16 storage), accumulation
+ * fp32 on v_mfma_f32_32x32x16_bf16, folded-BN bias fp32, outputs rounded to nearest even.
+ * Same epilogues and semantics as pipnet_conv2d_nhwc_f32; w_packed: [Cout][Kp] bf16 with
+ * Kp = KH*KW*Cin rounded up to a multiple of 64 (taps [KH][KW][Cin], zero beyond).
+ * Cin % 8 == 0, Cout % 8 == 0, x / w / y / R 16-byte aligned. */
+int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                            const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                            const void* R, int epilogue, void* y, void* stream);
+
+/* MaxPool2d(k, stride, pad) on NHWC bf16 (C % 8 == 0). */
+int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k, int stride, int pad,
+                               void* y, void* stream);
+
+/* fp32 NCHW -> bf16 NHWC (round to nearest even), channels zero-padded to Cpad (% 8 == 0). */
+int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y, void* stream);
+
+/* pipnet_softmax_pool_f32 reading bf16 logits (fp32 softmax, fp32 proto / pooled out). */
+int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
+                             float* pooled, void* stream);
+
 /* ConvNeXt stem: Conv2d(3,96,k4,s4,bias) + LayerNorm2d(96, eps 1e-6)  (features.0).
  * x: [B,3,H,W] NCHW (the reference's own input layout), w: [96,3,4,4] as torch stores it,
  * y: [B,H/4,W/4,96] NHWC. */

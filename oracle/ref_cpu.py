@@ -99,6 +99,58 @@ def resnet50_features(x: Tensor, sd: SD, prefix: str) -> Tensor:
     return x
 
 
+def _bf(x: Tensor) -> Tensor:
+    """Round to bfloat16 (nearest even) and back to fp32."""
+    return x.to(torch.bfloat16).float()
+
+
+def _conv_bn_bf16(x: Tensor, sd: SD, wkey: str, bnq: str, stride: int = 1, padding: int = 0) -> Tensor:
+    """conv + eval BatchNorm of the bf16 build: BN folded in fp32 (w*g/sqrt(v+eps),
+    b - mu*g/sqrt(v+eps)), folded weight rounded to bf16, fp32 accumulation, fp32 bias."""
+    scale = sd[bnq + "weight"] / torch.sqrt(sd[bnq + "running_var"] + 1e-5)
+    w = _bf(sd[wkey] * scale.view(-1, 1, 1, 1))
+    b = sd[bnq + "bias"] - sd[bnq + "running_mean"] * scale
+    return F.conv2d(x, w, b, stride=stride, padding=padding)
+
+
+def resnet50_features_bf16(x: Tensor, sd: SD, prefix: str) -> Tensor:
+    """The bf16 build of resnet50_features (BASELINE C3; the reference itself is fp32 only,
+    so this restates the build's arithmetic -- input and every conv output rounded to
+    bf16, epilogue bias / residual / ReLU in fp32 before the rounding).  Returns fp32
+    tensors holding bf16 values."""
+    p = prefix
+    x = _bf(x)
+    x = _bf(F.relu(_conv_bn_bf16(x, sd, p + "conv1.weight", p + "bn1.", 2, 3)))
+    x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+    for li, (n, stride) in enumerate([(3, 1), (4, 2), (6, 1), (3, 1)]):
+        for j in range(n):
+            q = f"{p}layer{li + 1}.{j}."
+            s = stride if j == 0 else 1
+            idt = x
+            if (q + "downsample.0.weight") in sd:
+                idt = _bf(_conv_bn_bf16(x, sd, q + "downsample.0.weight", q + "downsample.1.", s))
+            y = _bf(F.relu(_conv_bn_bf16(x, sd, q + "conv1.weight", q + "bn1.")))
+            y = _bf(F.relu(_conv_bn_bf16(y, sd, q + "conv2.weight", q + "bn2.", s, 1)))
+            x = _bf(F.relu(_conv_bn_bf16(y, sd, q + "conv3.weight", q + "bn3.") + idt))
+    return x
+
+
+def pipnet_forward_bf16(xs: Tensor, sd: SD, cfg, inference: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
+    """pipnet_forward with the bf16 ResNet build (optional 1x1 add-on also bf16 with fp32
+    bias, rounded); softmax / pool / classifier in fp32 as in the build's head."""
+    if cfg.net != "resnet50":
+        raise ValueError("oracle: the bf16 build covers resnet50 only")
+    feats = resnet50_features_bf16(xs, sd, "_net.")
+    if getattr(cfg, "num_features", 0):
+        feats = _bf(F.conv2d(feats, _bf(sd["_add_on.0.weight"]), sd["_add_on.0.bias"]))
+    proto = torch.softmax(feats, dim=1)
+    pooled = torch.amax(proto, dim=(2, 3))
+    if inference:
+        pooled = torch.where(pooled < 0.1, 0.0, pooled)
+    out = non_neg_linear(pooled, sd["_classification.weight"], sd.get("_classification.bias"))
+    return proto, pooled, out
+
+
 def backbone(x: Tensor, sd: SD, cfg) -> Tensor:
     if "convnext" in cfg.net:
         return convnext_features(x, sd, "_net.", cfg.net, getattr(cfg, "use_mid_layers", False),

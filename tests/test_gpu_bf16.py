@@ -1,0 +1,144 @@
+"""bf16 ResNet build (BASELINE C3 "ResNet50 ... bf16 inference") through the C-ABI.
+
+Kernel level: against the same arithmetic restated in torch -- bf16-valued operands, fp32
+conv (fp64 here), fp32 bias / residual / ReLU, one rounding to bf16.  The only freedom
+left is the fp32 accumulation order, so an output may differ from the restatement by one
+bf16 rounding step where the fp32 value sits next to a rounding boundary: tolerance 1
+bf16 ulp (2^-8 relative) + 1e-6, and >= 99 % of the elements bit-identical.
+
+End to end (golden C3 input): against oracle.ref_cpu.pipnet_forward_bf16 (the build's
+arithmetic) and against the reference's fp32 golden within the bf16 tolerance measured
+by the oracle itself (tests/test_oracle_golden.py::test_bf16_build_tolerance_vs_reference).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from count_pipnet_amd import _lib
+from count_pipnet_amd import kernels as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).double()
+
+
+def _close_bf16(out, ref):
+    out, ref = out.double(), ref.double()
+    err = (out - ref).abs()
+    assert torch.all(err <= ref.abs() * 2.0 ** -8 + 1e-6), err.max()
+    assert (err == 0).double().mean() >= 0.99, (err == 0).double().mean()
+
+
+@pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
+    (64, 64, 14, 1, 1, 0, _lib.EPI_BIAS_RELU),          # 1x1 dense
+    (256, 128, 13, 1, 2, 0, _lib.EPI_BIAS),             # 1x1 stride 2 (downsample)
+    (64, 64, 15, 3, 1, 1, _lib.EPI_BIAS_RELU),          # 3x3
+    (128, 128, 16, 3, 2, 1, _lib.EPI_BIAS_RELU),        # 3x3 stride 2
+    (64, 256, 9, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU),    # bottleneck conv3 + identity
+    (8, 64, 30, 7, 2, 3, _lib.EPI_BIAS_RELU),           # stem 7x7 (K 392 -> 448 padded)
+    (24, 72, 11, 3, 1, 1, _lib.EPI_NONE),               # K = 216 (not a 64 multiple), N = 72
+    (512, 2048, 7, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU),  # layer4 conv3
+])
+def test_conv2d_nhwc_bf16(gpu, cin, cout, h, k, s, pad, epi):
+    g = torch.Generator().manual_seed(cin * 3 + cout + h * 5 + k)
+    x = _bf(torch.randn(3, cin, h, h, generator=g).abs() if epi else torch.randn(3, cin, h, h, generator=g))
+    w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    wb = _bf(w)
+    b = torch.randn(cout, generator=g).double()
+    y = F.conv2d(x, wb, b if epi != _lib.EPI_NONE else None, stride=s, padding=pad)
+    r = _bf(torch.randn(*y.shape, generator=g))
+    if epi == _lib.EPI_BIAS_RELU:
+        y = torch.relu(y)
+    if epi == _lib.EPI_BIAS_RESID_RELU:
+        y = torch.relu(y + r)
+    ref = _bf(y.float()).permute(0, 2, 3, 1)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu)  # noqa: E731
+    wp = K.pack_conv_weight_bf16(w.permute(0, 2, 3, 1).contiguous().to(gpu))
+    out = K.conv2d_nhwc_bf16(nhwc(x), wp, k, k, b.float().to(gpu) if epi != _lib.EPI_NONE else None, s, pad, epi,
+                             nhwc(r) if epi == _lib.EPI_BIAS_RESID_RELU else None)
+    torch.cuda.synchronize()
+    assert out.dtype == torch.bfloat16 and tuple(out.shape) == tuple(ref.shape)
+    _close_bf16(out.cpu(), ref)
+
+
+def test_conv_bf16_layout_asymmetric(gpu):
+    """1x1 conv with identity input and an asymmetric exactly-representable weight: any
+    transposed or mis-swizzled fragment shows up as a wrong element."""
+    n = 128
+    x = torch.eye(n).view(1, n, 1, n)                                # [1, H=n, W=1, C=n] NHWC: pixel i = e_i
+    w = ((torch.arange(n * n) % 251) / 8.0).view(n, n)              # multiples of 1/8 < 32: exact in bf16
+    out = K.conv2d_nhwc_bf16(x.contiguous().to(torch.bfloat16).to(gpu),
+                             K.pack_conv_weight_bf16(w.view(n, 1, 1, n).to(gpu)), 1, 1, None, 1, 0, _lib.EPI_NONE)
+    assert torch.equal(out.float().cpu().view(n, n), w.t().contiguous())
+
+
+def test_maxpool_relayout_softmax_bf16(gpu):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 64, 23, 23, generator=g).to(torch.bfloat16)
+    out = K.maxpool2d_nhwc_bf16(x.permute(0, 2, 3, 1).contiguous().to(gpu), 3, 2, 1).cpu()
+    assert torch.equal(out, F.max_pool2d(x.float(), 3, 2, 1).to(torch.bfloat16).permute(0, 2, 3, 1))
+    xin = torch.randn(2, 3, 17, 19, generator=g)
+    y = K.nchw_to_nhwc_bf16(xin.to(gpu), 8).cpu()
+    assert torch.equal(y[..., :3], xin.to(torch.bfloat16).permute(0, 2, 3, 1)) and torch.all(y[..., 3:] == 0)
+    for p in (2048, 200):
+        f = (torch.randn(2, 5, 7, p, generator=g) * 3).to(torch.bfloat16)
+        proto, pooled = K.softmax_pool_bf16(f.to(gpu), 0)
+        ref = torch.softmax(f.double(), dim=-1)
+        assert torch.allclose(proto.double().cpu(), ref, atol=1e-6, rtol=1e-5)
+        assert torch.allclose(pooled.double().cpu(), ref.amax(dim=(1, 2)), atol=1e-6, rtol=1e-5)
+
+
+def _c3_bf16(gpu, num_features=0):
+    from golden_util import golden_args, golden_inputs, golden_state_dict, load_golden
+    from model_util import build_model
+    from count_pipnet_amd.pipnet import set_hip_dtype
+    meta, rec = load_golden("c3_pipnet_resnet50")
+    net = set_hip_dtype(build_model(meta), torch.bfloat16).to(gpu)
+    return meta, rec, net, golden_inputs(meta), golden_state_dict(meta), golden_args(meta)
+
+
+def test_c3_bf16_matches_bf16_oracle_and_reference(gpu):
+    from oracle import ref_cpu
+    meta, rec, net, xs, sd, args = _c3_bf16(gpu)
+    torch.set_num_threads(8)
+    with torch.no_grad():
+        proto, pooled, out = net(xs.to(gpu), inference=True)
+        r_proto, r_pooled, r_out = ref_cpu.pipnet_forward_bf16(xs, sd, args, inference=True)
+    proto, pooled, out = proto.float().cpu(), pooled.cpu(), out.cpu()
+    assert proto.dtype == torch.float32 and tuple(proto.shape) == tuple(r_proto.shape)
+    # vs the build's arithmetic restated on the CPU
+    near = (r_pooled - 0.1).abs() < 1e-2
+    assert torch.all((pooled - r_pooled).abs()[~near] <= 1e-2), (pooled - r_pooled).abs().max()
+    scale = r_out.abs().max().clamp(min=1.0)
+    if not near.any():
+        assert (out - r_out).abs().max() <= 1e-2 * scale
+    assert (proto.amax(dim=(2, 3)) - r_proto.amax(dim=(2, 3))).abs().max() <= 1e-2
+    # vs the reference's fp32 outputs (golden): bf16 tolerance
+    g_pooled, g_out = torch.from_numpy(rec["inf_pooled"]), torch.from_numpy(rec["inf_out"])
+    gnear = (g_pooled - 0.1).abs() < 5e-2
+    assert torch.all((pooled - g_pooled).abs()[~gnear] <= 5e-2)
+    gs = g_out.abs().max().clamp(min=1.0)
+    assert (out - g_out).abs().max() <= 5e-2 * gs
+    srt = g_out.sort(dim=1).values
+    decisive = (srt[:, -1] - srt[:, -2]) > 0.1 * gs
+    assert torch.equal(out.argmax(1)[decisive], g_out.argmax(1)[decisive])
+
+
+def test_c3_bf16_full_batch_properties(gpu):
+    """BASELINE C3 size (bs=128, 224x224): shapes, softmax normalisation, pooled = max of
+    proto, per-image determinism (image 0 alone == image 0 in the batch)."""
+    from count_pipnet_amd.synthetic import synth_images
+    meta, rec, net, _, _, _ = _c3_bf16(gpu)
+    xs = synth_images(128, 224, seed=11).to(gpu)
+    with torch.no_grad():
+        proto, pooled, out = net(xs, inference=False)
+        p1, pl1, o1 = net(xs[:1], inference=False)
+    assert tuple(proto.shape) == (128, 2048, 28, 28) and tuple(out.shape) == (128, 200)
+    s = proto.sum(dim=1)
+    assert torch.allclose(s, torch.ones_like(s), atol=1e-4)
+    assert torch.equal(pooled, proto.amax(dim=(2, 3)))
+    assert torch.equal(pl1[0], pooled[0]) and torch.equal(o1[0], out[0])
+    assert torch.isfinite(out).all()

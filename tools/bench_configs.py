@@ -1,7 +1,7 @@
 """Throughput of the non-headline BASELINE configs on one GPU (bench.py measures configs[1]).
 
   C1  CountPIPNet identity.yaml, 64x64, bs=16          (the reference's CPU case; here on HIP)
-  C3  PIP-Net ResNet50 224x224, bs=128, fp32           (BASELINE names bf16; fp32 here = exact)
+  C3  PIP-Net ResNet50 224x224, bs=128, bf16 (BASELINE C3) and fp32 (exact reference arithmetic)
   C5  CountPIPNet bilinear 2048 prototypes, 128x128, 64 images per GPU (bs=256 over 4 GPUs)
   C2' PIP-Net ConvNeXt-tiny-13 224x224, bs=64          (the 13x13 variant)
 
@@ -29,8 +29,10 @@ CONFIGS = {
                args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=16,
                          activation="gumbel_softmax", intermediate_layer="identity", max_count=3, use_ste=True,
                          bias=False), gflop=0.2495),
-    "c3": dict(model="pipnet", batch=128, size=224, classes=200, args=dict(net="resnet50", num_features=0, bias=False),
-               gflop=38.16),
+    "c3": dict(model="pipnet", batch=128, size=224, classes=200, args=dict(net="resnet50", num_features=0, bias=False,
+                                                                           hip_dtype="bf16"), gflop=38.16),
+    "c3_fp32": dict(model="pipnet", batch=128, size=224, classes=200,
+                    args=dict(net="resnet50", num_features=0, bias=False), gflop=38.16),
     "c5": dict(model="count", batch=64, size=128, classes=9,
                args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=2048,
                          activation="gumbel_softmax", intermediate_layer="bilinear", max_count=3, use_ste=True,
@@ -74,10 +76,11 @@ def main():
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
         ips = cfg["batch"] * a.steps / el
+        dt = cfg["args"].get("hip_dtype", "f32")
+        peak = 2500.0 if dt == "bf16" else 157.3
         print(json.dumps(dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
-                              image_size=cfg["size"], dtype="f32",
-                              model_tflops=ips * cfg["gflop"] / 1e3,
-                              model_frac_of_f32_peak=ips * cfg["gflop"] / 1e3 / 157.3)), flush=True)
+                              image_size=cfg["size"], dtype=dt, model_tflops=ips * cfg["gflop"] / 1e3,
+                              model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak)), flush=True)
         del net, xs
         torch.cuda.empty_cache()
 
