@@ -31,9 +31,12 @@ SIGNATURES = {
     "pipnet_maxpool2d_nhwc_f32": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_f32": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_conv2d_nhwc_bf16": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, P],
+    "pipnet_conv2d_nhwc_bf16_tile": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, I32, P],
     "pipnet_maxpool2d_nhwc_bf16": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_bf16": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_softmax_pool_bf16": [P, I32, I32, I32, I32, P, P, P],
+    "pipnet_eval_batch_f32": [P, P, P, I32, I32, I32, P, P, F32, P, P, P, P, P, P, P],
+    "pipnet_weight_sparsify_f32": [P, I64, F32, P],
     "pipnet_dwconv7_ln_f32": [P, I32, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_layernorm_f32": [P, I64, I32, P, P, P, P],
     "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],

@@ -15,18 +15,35 @@ int choose_group_m(int K) {
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 
+using CfgS = Cfg<2, 2, 1, 2>;   //  64 x 128, 256 threads, 48 KiB LDS, 3 workgroups / CU
+using CfgM = Cfg<2, 2, 2, 2>;   // 128 x 128, 256 threads, 64 KiB LDS, 2 workgroups / CU
+using CfgL = Cfg<2, 4, 4, 2>;   // 256 x 256, 512 threads, 128 KiB LDS, 1 workgroup / CU
+
+// Tile choice: the largest tile that still gives every CU at least one workgroup (larger
+// tiles halve the L2 -> LDS bytes per MFMA: 128x128 needs ~64 B/clk/CU at the MFMA rate,
+// the L2's whole bandwidth; 256x256 needs 32).  Mirrored by kernels.py:bf16_conv_kernel_name.
+int conv_variant(int M, int N) {
+  const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  if (N >= 256 && tl >= 256) return 2;
+  if (tm >= 512) return 1;
+  return 0;
+}
+
 template <int ALOAD>
-int launch_conv(ConvParams& p, int epi, hipStream_t s) {
-  p.nt = (p.N + BN - 1) / BN;
+int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
+  if (v < 0) v = conv_variant(p.M, p.N);
+  if (v > 2) return PIPNET_ERR_ARG;
+  const int bm = v == 2 ? 256 : (v == 1 ? 128 : 64), bn = v == 2 ? 256 : 128;
+  p.nt = (p.N + bn - 1) / bn;
+  p.mt = (p.M + bm - 1) / bm;
   p.group_m = choose_group_m(p.K);
-  // 128-row tiles unless that leaves fewer than two workgroups per CU
-  const bool tm2 = (int64_t)((p.M + 127) / 128) * p.nt >= 512;
-  p.mt = tm2 ? (p.M + 127) / 128 : (p.M + 63) / 64;
-  const dim3 grid(p.mt * p.nt), block(NTHREADS);
-#define PIPNET_BF_CASE(E)                                                                        \
-  case E:                                                                                       \
-    if (tm2) hipLaunchKernelGGL((conv_bf16_kernel<2, E, ALOAD, 2>), grid, block, 0, s, p);      \
-    else hipLaunchKernelGGL((conv_bf16_kernel<1, E, ALOAD, 3>), grid, block, 0, s, p);          \
+  const dim3 grid(p.mt * p.nt);
+#define PIPNET_BF_CASE(E)                                                                            \
+  case E:                                                                                           \
+    if (v == 2) hipLaunchKernelGGL((conv_bf16_kernel<CfgL, E, ALOAD, 1>), grid, dim3(512), 0, s, p);  \
+    else if (v == 1) hipLaunchKernelGGL((conv_bf16_kernel<CfgM, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
+    else hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p);        \
     break;
   switch (epi) {
     PIPNET_BF_CASE(PIPNET_EPI_NONE)
@@ -94,9 +111,9 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_bf16_kernel(const bf16* __re
 
 }  // namespace
 
-extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const void* w_packed,
-                                       const float* bias, int Cout, int KH, int KW, int stride, int pad,
-                                       const void* R, int epilogue, void* y, void* stream) {
+extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                                            const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                            const void* R, int epilogue, void* y, int tile, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || (Cin & 7) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
       stride <= 0 || pad < 0)
     return PIPNET_ERR_ARG;
@@ -125,9 +142,16 @@ extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int C
   p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
     p.lda = Cin;
-    return launch_conv<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
+    return launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream);
   }
-  return launch_conv<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
+  return launch_conv<ALOAD_CONV>(p, epilogue, tile, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                                       const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                       const void* R, int epilogue, void* y, void* stream) {
+  return pipnet_conv2d_nhwc_bf16_tile(x, B, H, W, Cin, w_packed, bias, Cout, KH, KW, stride, pad, R, epilogue, y, -1,
+                                      stream);
 }
 
 extern "C" int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y,

@@ -25,7 +25,7 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 64, BN = 128, NTHREADS = 256, NWAVES = 4;
+constexpr int BK = 64;
 constexpr int CHUNKS = 8, ROWS_PER_DMA = 8;   // 128-B rows; one 1-KiB DMA fills 8 rows
 
 struct ConvParams {
@@ -85,42 +85,48 @@ PIPNET_DEV const void* a_ptr(const ConvParams& p, const ARow& r, int k) {
 
 PIPNET_DEV int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
 
-template <int TM>
-struct Geo {
-  static constexpr int BMT = 64 * TM;
+// Workgroup tile: WGM x WGN waves, each wave TM x TN MFMA 32x32 tiles.
+//   <2,2,2,2> 128x128 (256 threads), <2,2,1,2> 64x128, <2,4,4,2> 256x256 (512 threads).
+template <int WGM_, int WGN_, int TM_, int TN_>
+struct Cfg {
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_;
+  static constexpr int NWAVES = WGM * WGN, NTHREADS = 64 * NWAVES;
+  static constexpr int BMT = WGM * 32 * TM, BNT = WGN * 32 * TN;
   static constexpr int A_DMA = BMT / ROWS_PER_DMA / NWAVES;
-  static constexpr int B_DMA = BN / ROWS_PER_DMA / NWAVES;
-  static constexpr int TILE_ELEMS = (BMT + BN) * BK;   // bf16 elements of one stage
+  static constexpr int B_DMA = BNT / ROWS_PER_DMA / NWAVES;
+  static constexpr int TILE_ELEMS = (BMT + BNT) * BK;   // bf16 elements of one stage
+  static_assert(A_DMA * ROWS_PER_DMA * NWAVES == BMT && B_DMA * ROWS_PER_DMA * NWAVES == BNT, "DMA split");
 };
 
-template <int TM>
+template <class C>
 struct Frag {
-  bf16x8 a[TM], b[2];
+  bf16x8 a[C::TM], b[C::TN];
 };
-template <int TM>
-using Acc = f32x16[TM][2];
+template <class C>
+using Acc = f32x16[C::TM][C::TN];
 
-template <int TM>
-PIPNET_DEV void read_frag(Frag<TM>& f, const bf16* buf, int wm, int wn, int lr, int lh, int q) {
+template <class C>
+PIPNET_DEV void read_frag(Frag<C>& f, const bf16* buf, int wm, int wn, int lr, int lh, int q) {
   const int c = lh * 4 + q;
 #pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int ra = wm * 32 * TM + i * 32 + lr;
+  for (int i = 0; i < C::TM; ++i) {
+    const int ra = wm * 32 * C::TM + i * 32 + lr;
     f.a[i] = *reinterpret_cast<const bf16x8*>(buf + ra * BK + 8 * swz(ra, c));
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int rb = wn * 64 + j * 32 + lr;
-    f.b[j] = *reinterpret_cast<const bf16x8*>(buf + Geo<TM>::BMT * BK + rb * BK + 8 * swz(rb, c));
+  for (int j = 0; j < C::TN; ++j) {
+    const int rb = wn * 32 * C::TN + j * 32 + lr;
+    f.b[j] = *reinterpret_cast<const bf16x8*>(buf + C::BMT * BK + rb * BK + 8 * swz(rb, c));
   }
 }
 
-template <int TM>
-PIPNET_DEV void mfma_frag(Acc<TM>& acc, const Frag<TM>& f) {
+template <class C>
+PIPNET_DEV void mfma_frag(Acc<C>& acc, const Frag<C>& f) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+    for (int j = 0; j < C::TN; ++j)
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
 }
 
 PIPNET_DEV void dma16(const void* src, bf16* lds_base) {
@@ -128,7 +134,7 @@ PIPNET_DEV void dma16(const void* src, bf16* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
-PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int& m0, int& n0) {
+PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int bn, int& m0, int& n0) {
   const int nwg = p.mt * p.nt;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int gm = p.group_m;
@@ -137,39 +143,40 @@ PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int& m0, int& n0) {
   const int gsz = min(p.mt - first_m, gm);
   const int in_group = tile - group * gm * p.nt;
   m0 = (first_m + in_group % gsz) * bm;
-  n0 = (in_group / gsz) * BN;
+  n0 = (in_group / gsz) * bn;
 }
 
 PIPNET_DEV u32x4 as_u32x4(const bf16x8& v) { return __builtin_bit_cast(u32x4, v); }
 
-// Epilogue: each wave re-lays its 32x64 fp32 accumulator slice through LDS (rows padded to
-// 68 floats: the 16-B reads of 8 consecutive lanes then cover all 64 banks), then every
+// Epilogue: each wave re-lays its 32 x (TN*32) fp32 accumulator slice through LDS (rows
+// padded by 4 floats: the 16-B reads of one row's lanes then cover all 64 banks), then every
 // lane finishes 8 consecutive channels of one pixel -- bias, residual (one 16-B bf16
 // load, all issued before the first store), ReLU, round-to-nearest-even to bf16
 // (v_cvt_pk_bf16_f32), one 16-B store.  Needs N % 8 == 0 and 16-B aligned C / R rows.
-constexpr int EPI_LD = 68;
-
-template <int EPI, int TM>
-PIPNET_DEV void epilogue(const ConvParams& p, const Acc<TM>& acc, float* smem, int m0, int n0, int wm, int wn,
+template <int EPI, class C>
+PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, int m0, int n0, int wm, int wn,
                          int lane, int wid) {
+  constexpr int TM = C::TM, TN = C::TN, LD = TN * 32 + 4;
   constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
-  float* wt = smem + wid * 32 * EPI_LD;
+  // a lane finishes 8 channels; CPR lanes cover one row of the wave's TN*32 columns
+  constexpr int CPR = TN * 4, RPI = 64 / CPR, NIT = 32 / RPI;
+  float* wt = smem + wid * 32 * LD;
   const int lr = lane & 31, lh = lane >> 5;
-  const int c8 = lane & 7;
-  const int n = n0 + wn * 64 + 8 * c8;
+  const int c8 = lane % CPR;
+  const int n = n0 + wn * 32 * TN + 8 * c8;
   const bool nok = n < p.N;
   f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
     b0 = ld4(p.bias + n);
     b1 = ld4(p.bias + n + 4);
   }
-  bf16x8 r[TM][4];
+  bf16x8 r[TM][NIT];
   if (HAS_R) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int m = min(m0 + wm * 32 * TM + i * 32 + it * 8 + (lane >> 3), p.M - 1);
+      for (int it = 0; it < NIT; ++it) {
+        const int m = min(m0 + wm * 32 * TM + i * 32 + it * RPI + lane / CPR, p.M - 1);
         if (nok) r[i][it] = *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + n);
       }
   }
@@ -177,15 +184,15 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<TM>& acc, float* smem, i
   for (int i = 0; i < TM; ++i) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * EPI_LD + j * 32 + lr] = acc[i][j][v];
+      for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * LD + j * 32 + lr] = acc[i][j][v];
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int row = it * 8 + (lane >> 3);
+    for (int it = 0; it < NIT; ++it) {
+      const int row = it * RPI + lane / CPR;
       const int m = m0 + wm * 32 * TM + i * 32 + row;
-      f32x4 x0 = ld4(wt + row * EPI_LD + 8 * c8), x1 = ld4(wt + row * EPI_LD + 8 * c8 + 4);
+      f32x4 x0 = ld4(wt + row * LD + 8 * c8), x1 = ld4(wt + row * LD + 8 * c8 + 4);
       x0 += b0;
       x1 += b1;
       if (HAS_R) {
@@ -213,78 +220,78 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<TM>& acc, float* smem, i
   }
 }
 
-// TM = 1: 64x128 tiles, TM = 2: 128x128; 4 waves in 2x2, 2 LDS stages, one barrier per
-// 64-deep K tile, fragments software-pipelined over the tile's 4 chunk groups.
-template <int TM, int EPI, int ALOAD, int MINB>
-__global__ __launch_bounds__(NTHREADS, MINB) void conv_bf16_kernel(ConvParams p) {
-  using G = Geo<TM>;
+// 2 LDS stages, one barrier per 64-deep K tile, fragments software-pipelined over the
+// tile's 4 chunk groups (chunk group q of half-wave h = k 32h + 8q .. +7).
+template <class C, int EPI, int ALOAD, int MINB>
+__global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams p) {
   constexpr int NS = 2;
-  __shared__ __attribute__((aligned(16))) bf16 smem[NS * G::TILE_ELEMS];
-  static_assert(NS * G::TILE_ELEMS * 2 >= NWAVES * 32 * EPI_LD * 4, "epilogue LDS");
+  constexpr int NWAVES = C::NWAVES;
+  __shared__ __attribute__((aligned(16))) bf16 smem[NS * C::TILE_ELEMS];
+  static_assert(NS * C::TILE_ELEMS * 2 >= NWAVES * 32 * (C::TN * 32 + 4) * 4, "epilogue LDS");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / C::WGN, wn = wid % C::WGN;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, G::BMT, m0, n0);
+  tile_coords(p, C::BMT, C::BNT, m0, n0);
   const int nk = p.K / BK;
 
   const int drow = lane / CHUNKS;
-  ARow arow[G::A_DMA];
-  int achunk[G::A_DMA];
-  const bf16* wsrc[G::B_DMA];
+  ARow arow[C::A_DMA];
+  int achunk[C::A_DMA];
+  const bf16* wsrc[C::B_DMA];
 #pragma unroll
-  for (int i = 0; i < G::A_DMA; ++i) {
+  for (int i = 0; i < C::A_DMA; ++i) {
     const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
     achunk[i] = 8 * swz(row, lane % CHUNKS);
     arow[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
   }
 #pragma unroll
-  for (int i = 0; i < G::B_DMA; ++i) {
+  for (int i = 0; i < C::B_DMA; ++i) {
     const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
     wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * swz(row, lane % CHUNKS);
   }
   auto stage = [&](int kt, int buf) {
-    bf16* base = smem + buf * G::TILE_ELEMS;
+    bf16* base = smem + buf * C::TILE_ELEMS;
     const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < G::A_DMA; ++i)
+    for (int i = 0; i < C::A_DMA; ++i)
       dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
 #pragma unroll
-    for (int i = 0; i < G::B_DMA; ++i)
-      dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
+    for (int i = 0; i < C::B_DMA; ++i)
+      dma16(wsrc[i] + k0, base + C::BMT * BK + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
   };
 
-  Acc<TM> acc;
+  Acc<C> acc;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+  for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < C::TN; ++j)
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
   stage(0, 0);
   __syncthreads();
-  Frag<TM> fa, fb;
-  read_frag<TM>(fa, smem, wm, wn, lr, lh, 0);
+  Frag<C> fa, fb;
+  read_frag<C>(fa, smem, wm, wn, lr, lh, 0);
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const bf16* buf = smem + cur * G::TILE_ELEMS;
+    const bf16* buf = smem + cur * C::TILE_ELEMS;
     if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    read_frag<TM>(fb, buf, wm, wn, lr, lh, 1);
-    mfma_frag<TM>(acc, fa);
-    read_frag<TM>(fa, buf, wm, wn, lr, lh, 2);
-    mfma_frag<TM>(acc, fb);
-    read_frag<TM>(fb, buf, wm, wn, lr, lh, 3);
-    mfma_frag<TM>(acc, fa);
+    read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
+    mfma_frag<C>(acc, fa);
+    read_frag<C>(fa, buf, wm, wn, lr, lh, 2);
+    mfma_frag<C>(acc, fb);
+    read_frag<C>(fb, buf, wm, wn, lr, lh, 3);
+    mfma_frag<C>(acc, fa);
     __syncthreads();                                     // tile kt+1 landed, tile kt read
-    if (kt + 1 < nk) read_frag<TM>(fa, smem + (cur ^ 1) * G::TILE_ELEMS, wm, wn, lr, lh, 0);
-    mfma_frag<TM>(acc, fb);
+    if (kt + 1 < nk) read_frag<C>(fa, smem + (cur ^ 1) * C::TILE_ELEMS, wm, wn, lr, lh, 0);
+    mfma_frag<C>(acc, fb);
     cur ^= 1;
   }
-  epilogue<EPI, TM>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
+  epilogue<EPI, C>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
 }
 
 }  // namespace pipnet_bf16

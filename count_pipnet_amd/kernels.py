@@ -47,7 +47,7 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
 def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
     """K slabs for short-M GEMMs: enough workgroups to cover every CU at least once, each
     slab >= 8 K-tiles of 32 (the Bilinear intermediate at M = batch has only 48 tiles)."""
-    if n % 4 or k % 32:
+    if n % 4 or k % 32 or m > 512:     # backbone GEMMs (M = pixels) stay batch-invariant
         return 1
     tiles = -(-m // 64) * -(-n // 128)
     if tiles >= cus:
@@ -167,11 +167,22 @@ def _chk_bf(t: Tensor, what: str) -> None:
         raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
 
 
-def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int) -> str:
-    """rocprof name of the bf16 conv instantiation (mirrors launch_conv in csrc/conv_bf16.hip)."""
-    tm2 = -(-m // 128) * -(-n // 128) >= 512
-    return (f"pipnet_bf16::conv_bf16_kernel<2, {epilogue}, {aload}, 2>" if tm2
-            else f"pipnet_bf16::conv_bf16_kernel<1, {epilogue}, {aload}, 3>")
+def bf16_conv_tile(m: int, n: int) -> int:
+    """Workgroup tile the library picks (mirrors conv_variant in csrc/conv_bf16.hip):
+    0 = 64x128, 1 = 128x128, 2 = 256x256."""
+    if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
+        return 2
+    return 1 if -(-m // 128) * -(-n // 128) >= 512 else 0
+
+
+_BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2>", 2),
+             2: ("pipnet_bf16::Cfg<2, 4, 4, 2>", 1)}
+
+
+def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1) -> str:
+    """rocprof name of the bf16 conv instantiation."""
+    cfg, minb = _BF16_CFG[bf16_conv_tile(m, n) if tile < 0 else tile]
+    return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}>"
 
 
 def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
@@ -185,8 +196,9 @@ def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
 
 
 def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Optional[Tensor], stride: int,
-                     pad: int, epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None) -> Tensor:
-    """NHWC bf16 implicit-GEMM convolution; w_packed from pack_conv_weight_bf16; bias fp32."""
+                     pad: int, epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None, tile: int = -1) -> Tensor:
+    """NHWC bf16 implicit-GEMM convolution; w_packed from pack_conv_weight_bf16; bias fp32;
+    tile -1 = automatic, 0/1/2 = forced 64x128 / 128x128 / 256x256 workgroup tile."""
     _chk_bf(x, "conv input")
     _chk_bf(w_packed, "conv weight")
     if r is not None:
@@ -202,9 +214,10 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     y = torch.empty((b, oh, ow, cout), device=x.device, dtype=torch.bfloat16)
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload), 2.0 * m * cout * k,
-            lambda: _lib.call("pipnet_conv2d_nhwc_bf16", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
-                              _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), _stream(x)))
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile), 2.0 * m * cout * k,
+            lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
+                              _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), tile,
+                              _stream(x)))
     return y
 
 
@@ -325,3 +338,39 @@ def count_encode(x: Tensor, c: int, kind: int, do_round: bool, w: Optional[Tenso
     _lib.call("pipnet_count_encode_f32", x.data_ptr(), b, p, c, kind, int(do_round), _ptr(w), out.data_ptr(),
               _stream(x))
     return out
+
+
+# ---- eval_pipnet metric loop ------------------------------------------------------------
+
+def weight_sparsify_(w: Tensor, delta: float = 1e-3) -> Tensor:
+    """In place: w = max(w - delta, 0) (pipnet/test.py:73)."""
+    _chk(w, "classification weight")
+    _lib.call("pipnet_weight_sparsify_f32", w.data_ptr(), w.numel(), delta, _stream(w))
+    return w
+
+
+def eval_batch(pooled: Tensor, out: Tensor, w: Tensor, ys: Tensor, multiplier: Optional[Tensor], thr: float,
+               cm: Tensor, acc: Tensor, abstained: Tensor) -> Tuple[Tensor, Tensor]:
+    """One eval_pipnet batch on the device; accumulates into cm [K,K] int64, acc [5] fp64,
+    abstained [1] int64.  Returns (ys_pred [B] int32, score [B] fp32)."""
+    _chk(pooled, "pooled")
+    _chk(out, "logits")
+    _chk(w, "prototype-class weights")
+    b, p = pooled.shape
+    k = out.shape[1]
+    if tuple(w.shape) != (k, p) or out.shape[0] != b or ys.shape != (b,):
+        raise RuntimeError(f"eval_batch: shapes pooled {tuple(pooled.shape)}, out {tuple(out.shape)}, "
+                           f"w {tuple(w.shape)}, ys {tuple(ys.shape)} disagree")
+    if not (ys.is_cuda and ys.dtype == torch.int64 and ys.is_contiguous()):
+        raise RuntimeError("eval_batch: labels must be a contiguous int64 device tensor")
+    if cm.dtype != torch.int64 or acc.dtype != torch.float64 or abstained.dtype != torch.int64:
+        raise RuntimeError("eval_batch: accumulator dtypes are int64 / float64 / int64")
+    if multiplier is not None:
+        _chk(multiplier, "normalization multiplier")
+    ys_pred = torch.empty(b, device=out.device, dtype=torch.int32)
+    score = torch.empty(b, device=out.device, dtype=torch.float32)
+    ws = torch.empty(5 * b + k, device=out.device, dtype=torch.int32)
+    _lib.call("pipnet_eval_batch_f32", pooled.data_ptr(), out.data_ptr(), w.data_ptr(), b, p, k, ys.data_ptr(),
+              _ptr(multiplier), thr, ys_pred.data_ptr(), score.data_ptr(), cm.data_ptr(), acc.data_ptr(),
+              abstained.data_ptr(), ws.data_ptr(), _stream(out))
+    return ys_pred, score

@@ -99,6 +99,12 @@ int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const v
                             const float* bias, int Cout, int KH, int KW, int stride, int pad,
                             const void* R, int epilogue, void* y, void* stream);
 
+/* Same, with the workgroup tile forced (tuning / tests): tile 0 = 64x128, 1 = 128x128,
+ * 2 = 256x256, -1 = automatic (what pipnet_conv2d_nhwc_bf16 uses). */
+int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                                 const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                 const void* R, int epilogue, void* y, int tile, void* stream);
+
 /* MaxPool2d(k, stride, pad) on NHWC bf16 (C % 8 == 0). */
 int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k, int stride, int pad,
                                void* y, void* stream);
@@ -109,6 +115,24 @@ int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpa
 /* pipnet_softmax_pool_f32 reading bf16 logits (fp32 softmax, fp32 proto / pooled out). */
 int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
                              float* pooled, void* stream);
+
+/* ---- eval_pipnet metric loop (pipnet/test.py:67-131,266-319) -------
+ * One evaluation batch, entirely on the device (no host sync):
+ *   pooled [B,P] (clamped presence / counts), out [B,K] logits, W [K,P] the prototype->class
+ *   weights the reference multiplies with (PIP-Net: the sparsified classification weight;
+ *   CountPIPNet: get_prototype_importance_per_class stacked), ys [B] int64 labels,
+ *   multiplier -> normalization_multiplier (device scalar, may be NULL = 1), thr = 1e-3.
+ * Writes ys_pred [B] (torch.max index) and score [B] (amax softmax(log1p(out^m))); adds into
+ * cm [K,K] int64 (cm[y][pred]), acc[5] fp64 running sums of the per-batch means
+ * {true-class local size, all-class local size, prototypes per class, almost-nonzeros,
+ * top-1}, *abstained (images whose max logit is 0).  workspace: int32 [5B + K]. */
+int pipnet_eval_batch_f32(const float* pooled, const float* out, const float* W, int B, int P, int K,
+                          const int64_t* ys, const float* multiplier, float thr, int32_t* ys_pred,
+                          float* score, int64_t* cm, double* acc, int64_t* abstained, int32_t* workspace,
+                          void* stream);
+
+/* In-place classifier sparsification of eval_pipnet (test.py:71-73): w = max(w - delta, 0). */
+int pipnet_weight_sparsify_f32(float* w, int64_t n, float delta, void* stream);
 
 /* ConvNeXt stem: Conv2d(3,96,k4,s4,bias) + LayerNorm2d(96, eps 1e-6)  (features.0).
  * x: [B,3,H,W] NCHW (the reference's own input layout), w: [96,3,4,4] as torch stores it,

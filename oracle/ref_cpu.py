@@ -265,3 +265,49 @@ def gflop_per_image(cfg, image_size: int) -> float:
     if nf:
         flops += 2.0 * h * h * c * nf
     return flops / 1e9
+
+
+# ---- eval_pipnet metric loop (pipnet/test.py:67-131, 278-319) -------------------------------
+
+def eval_batch_metrics(pooled: Tensor, out: Tensor, w: Tensor, ys: Tensor, multiplier: float,
+                       thr: float = 1e-3) -> dict:
+    """The per-batch body of eval_pipnet after the forward (test.py:77-131): returns the
+    values the reference accumulates (as Python floats, exactly as its ``.item()`` calls)
+    and the per-image predictions / confidences.  ``w`` [K, P] is the weight the
+    reference multiplies ``pooled`` with (classification weight or count importances)."""
+    max_out_score, ys_pred = torch.max(out, dim=1)
+    scores_conf = torch.amax(F.softmax(torch.log1p(out ** multiplier), dim=1), dim=1)
+    abstained = int(max_out_score.shape[0] - torch.count_nonzero(max_out_score))
+    scores = pooled * w.unsqueeze(1).repeat(1, pooled.shape[0], 1)          # [K, B, P]
+    relevant = torch.abs(scores) > thr
+    any_sizes = relevant.any(dim=0).sum(dim=1).float()
+    pred_sizes = torch.diagonal(torch.index_select(relevant.sum(dim=2).float(), 0, ys_pred))
+    ppc = torch.count_nonzero(torch.gt(torch.relu(scores - thr).mean(dim=1), 0.).float(), dim=1).float()
+    anz = torch.count_nonzero(torch.gt(torch.abs(pooled), thr).float(), dim=1).float()
+    _, pred = out.topk(1, 1, True, True)
+    top1 = (pred.t() == ys.unsqueeze(0)).reshape(-1).float()
+    return dict(pred_size=pred_sizes.mean(0).item(), any_size=any_sizes.mean(0).item(),
+                ppc=ppc.mean(0).item(), anz=anz.mean().item(), top1=torch.mean(top1).item(),
+                abstained=abstained, ys_pred=ys_pred, conf=scores_conf)
+
+
+def eval_loop(batches, num_classes: int, multiplier: float, thr: float = 1e-3) -> dict:
+    """Accumulate eval_batch_metrics over ``batches`` = [(pooled, out, w, ys)] like
+    eval_pipnet (test.py:136-157): running Python-float sums / number of batches."""
+    import numpy as np
+    cm = np.zeros((num_classes, num_classes), dtype=int)
+    s = dict(pred_size=0., any_size=0., ppc=0., anz=0., top1=0.)
+    abstained = 0
+    for pooled, out, w, ys in batches:
+        r = eval_batch_metrics(pooled, out, w, ys, multiplier, thr)
+        for k in s:
+            s[k] += r[k]
+        abstained += r["abstained"]
+        for yp, yt in zip(r["ys_pred"].tolist(), ys.tolist()):
+            cm[yt][yp] += 1
+    n = len(batches)
+    total = cm.sum()
+    return {"confusion_matrix": cm, "test_accuracy": (np.trace(cm) / total) if total else 1,
+            "top1_accuracy": s["top1"] / n, "local_size_for_true_class": s["pred_size"] / n,
+            "local_size_for_all_classes": s["any_size"] / n, "prototypes_per_class": s["ppc"] / n,
+            "almost_nonzeros": s["anz"] / n, "abstained": abstained}

@@ -14,7 +14,12 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def golden_names():
-    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz"))
+    """Forward golden cases (eval_* fixtures belong to the eval_pipnet metric loop)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and not f.startswith("eval_"))
+
+
+def eval_golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.startswith("eval_") and f.endswith(".npz"))
 
 
 def load_golden(name: str):
@@ -54,3 +59,15 @@ def proto_shape(meta, rec):
         return tuple(rec["inf_proto"].shape)
     hw = rec["inf_proto_pixmax"].shape[1:]
     return (c["batch"], p) + tuple(hw)
+
+
+def eval_loader_batches(size: int, num_classes: int, nb: int, bs: int, label_seed: int):
+    """The in-memory loader of the eval_* fixtures (tests/golden/gen_golden_eval.py):
+    nb batches of (synthetic images, seeded labels)."""
+    g = torch.Generator().manual_seed(label_seed)
+    out = []
+    for i in range(nb):
+        xs = synth_images(bs, size, seed=label_seed * 100 + i)
+        ys = torch.randint(0, num_classes, (bs,), generator=g)
+        out.append((xs, ys))
+    return out
