@@ -72,6 +72,87 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
   }
 }
 
+// bf16 logits (the C3 ResNet build, P = 2048): 16-B loads of 8 consecutive channels per
+// lane (vector j of lane l = channels 8l + 512j ..), 2 x 16-B fp32 stores, so one wave
+// instruction moves 1 KiB of logits / 2 KiB of proto (the lane-strided kernel above would
+// issue 2-byte loads here: 1.85 TB/s measured).  P % 8 == 0, P <= 512 NV.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+template <int NV, int MODE>
+__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const __bf16* __restrict__ feat, int HW,
+                                                                          int P, float* __restrict__ proto,
+                                                                          float* __restrict__ pooled) {
+  __shared__ float red[HEAD_THREADS / 64][NV * 512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  float racc[NV][8];
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) racc[j][e] = 0.f;
+  for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
+    const int pix = pix0 + pi;
+    if (pix >= HW) break;
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+    float v[NV][8];
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 8 * lane + 512 * j;
+      if (c < P) {
+        const bf16x8_t x = *reinterpret_cast<const bf16x8_t*>(feat + base + c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = (float)x[e], m = fmaxf(m, v[j][e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[j][e] = -INFINITY;
+      }
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[j][e] = 8 * lane + 512 * j < P ? expf(v[j][e] - m) : 0.f;
+        s += v[j][e];
+      }
+    const float inv = 1.0f / wave_sum(s);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 8 * lane + 512 * j;
+      if (c < P) {
+        f32x4 y0, y1;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y0[e] = v[j][e] * inv, y1[e] = v[j][4 + e] * inv;
+        st4(proto + base + c, y0);
+        st4(proto + base + c + 4, y1);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          racc[j][e] = MODE == 0 ? fmaxf(racc[j][e], y0[e]) : racc[j][e] + y0[e];
+          racc[j][4 + e] = MODE == 0 ? fmaxf(racc[j][4 + e], y1[e]) : racc[j][4 + e] + y1[e];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wv][8 * lane + 512 * j + e] = racc[j][e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
+    float r = red[0][c];
+#pragma unroll
+    for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
+    float* dst = pooled + (int64_t)b * P + c;
+    if (MODE == 0)
+      atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
+    else
+      atomicAdd(dst, r);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // NonNegLinear: grid (image, class block of 16); x' staged in LDS; each wave computes 4
 // classes at once (4 independent dot products in flight, float4 W reads).
@@ -284,7 +365,29 @@ extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, 
 
 extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
                                         float* pooled, void* stream) {
-  return softmax_pool_launch(reinterpret_cast<const __bf16*>(feat), B, HW, P, pool_mode, proto, pooled, stream);
+  const __bf16* f = reinterpret_cast<const __bf16*>(feat);
+  if (P % 8 || P > 2048 || !aligned16(feat) || !aligned16(proto))
+    return softmax_pool_launch(f, B, HW, P, pool_mode, proto, pooled, stream);
+  if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1) || !pooled) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(pooled, 0, sizeof(float) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+#define SPV_CALL(N)                                                                                            \
+  if (pool_mode == 0)                                                                                          \
+    hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
+  else                                                                                                         \
+    hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled);
+  if (P <= 512) {
+    SPV_CALL(1)
+  } else if (P <= 1024) {
+    SPV_CALL(2)
+  } else {
+    SPV_CALL(4)
+  }
+#undef SPV_CALL
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
 }
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,

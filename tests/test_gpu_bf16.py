@@ -110,12 +110,14 @@ def test_maxpool_relayout_softmax_bf16(gpu):
     xin = torch.randn(2, 3, 17, 19, generator=g)
     y = K.nchw_to_nhwc_bf16(xin.to(gpu), 8).cpu()
     assert torch.equal(y[..., :3], xin.to(torch.bfloat16).permute(0, 2, 3, 1)) and torch.all(y[..., 3:] == 0)
-    for p in (2048, 200):
+    for p in (2048, 200, 1000, 36):          # vectorised NV = 4 / 1 / 2, and the P % 8 != 0 fallback
         f = (torch.randn(2, 5, 7, p, generator=g) * 3).to(torch.bfloat16)
-        proto, pooled = K.softmax_pool_bf16(f.to(gpu), 0)
         ref = torch.softmax(f.double(), dim=-1)
-        assert torch.allclose(proto.double().cpu(), ref, atol=1e-6, rtol=1e-5)
-        assert torch.allclose(pooled.double().cpu(), ref.amax(dim=(1, 2)), atol=1e-6, rtol=1e-5)
+        for mode in (0, 1):
+            proto, pooled = K.softmax_pool_bf16(f.to(gpu), mode)
+            assert torch.allclose(proto.double().cpu(), ref, atol=1e-6, rtol=1e-5)
+            rp = ref.amax(dim=(1, 2)) if mode == 0 else ref.sum(dim=(1, 2))
+            assert torch.allclose(pooled.double().cpu(), rp, atol=1e-6, rtol=1e-5)
 
 
 def _c3_bf16(gpu, num_features=0):
