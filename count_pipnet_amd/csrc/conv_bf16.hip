@@ -15,26 +15,30 @@ int choose_group_m(int K) {
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 
-using CfgS = Cfg<2, 2, 1, 2>;   //  64 x 128, 256 threads, 48 KiB LDS, 3 workgroups / CU
-using CfgM = Cfg<2, 2, 2, 2>;   // 128 x 128, 256 threads, 64 KiB LDS, 2 workgroups / CU
-using CfgL = Cfg<2, 4, 4, 2>;   // 256 x 256, 512 threads, 128 KiB LDS, 1 workgroup / CU
+using CfgS = Cfg<2, 2, 1, 2>;          //  64 x 128, 256 threads, 48 KiB LDS, 3 workgroups / CU
+using CfgM = Cfg<2, 2, 2, 2>;          // 128 x 128, 256 threads, 64 KiB LDS, 2 workgroups / CU
+using CfgL = Cfg<2, 4, 4, 2>;          // 256 x 256, 512 threads, 128 KiB LDS, 1 workgroup / CU
+using CfgL4 = Cfg<2, 4, 4, 2, 32, 4>;  // 256 x 256, BK 32 x 4 stages (3 tiles in flight), 128 KiB
+using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2 workgroups / CU
 
 // Tile choice: the largest tile that still gives every CU at least one workgroup (larger
 // tiles halve the L2 -> LDS bytes per MFMA: 128x128 needs ~64 B/clk/CU at the MFMA rate,
-// the L2's whole bandwidth; 256x256 needs 32).  Mirrored by kernels.py:bf16_conv_kernel_name.
+// the L2's whole bandwidth; 256x256 needs 32), with 32-deep K tiles in 4 stages (+1..+30 %
+// over 64-deep x 2 on the ResNet50 shapes, profiles/r01/conv_bf16_tiles.log).  Mirrored by
+// kernels.py:bf16_conv_tile.
 int conv_variant(int M, int N) {
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  if (N >= 256 && tl >= 256) return 2;
-  if (tm >= 512) return 1;
+  if (N >= 256 && tl >= 256) return 3;
+  if (tm >= 512) return 4;
   return 0;
 }
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   if (v < 0) v = conv_variant(p.M, p.N);
-  if (v > 2) return PIPNET_ERR_ARG;
-  const int bm = v == 2 ? 256 : (v == 1 ? 128 : 64), bn = v == 2 ? 256 : 128;
+  if (v > 4) return PIPNET_ERR_ARG;
+  const int bm = (v == 2 || v == 3) ? 256 : (v == 0 ? 64 : 128), bn = (v == 2 || v == 3) ? 256 : 128;
   p.nt = (p.N + bn - 1) / bn;
   p.mt = (p.M + bm - 1) / bm;
   p.group_m = choose_group_m(p.K);
@@ -42,6 +46,8 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
 #define PIPNET_BF_CASE(E)                                                                            \
   case E:                                                                                           \
     if (v == 2) hipLaunchKernelGGL((conv_bf16_kernel<CfgL, E, ALOAD, 1>), grid, dim3(512), 0, s, p);  \
+    else if (v == 3) hipLaunchKernelGGL((conv_bf16_kernel<CfgL4, E, ALOAD, 1>), grid, dim3(512), 0, s, p); \
+    else if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else if (v == 1) hipLaunchKernelGGL((conv_bf16_kernel<CfgM, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p);        \
     break;
@@ -138,7 +144,7 @@ extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, 
   p.ldc = Cout;
   p.M = B * OH * OW; p.N = Cout;
   p.Kv = KH * KW * Cin;
-  p.K = (p.Kv + BK - 1) / BK * BK;
+  p.K = (p.Kv + KPAD - 1) / KPAD * KPAD;
   p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
     p.lda = Cin;

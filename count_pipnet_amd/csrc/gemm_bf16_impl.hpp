@@ -25,8 +25,7 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 64;
-constexpr int CHUNKS = 8, ROWS_PER_DMA = 8;   // 128-B rows; one 1-KiB DMA fills 8 rows
+constexpr int KPAD = 64;                      // packed weights: K rounded up to this
 
 struct ConvParams {
   const bf16* A;
@@ -72,7 +71,7 @@ PIPNET_DEV ARow a_row(const ConvParams& p, int m) {
 // Address of A[m][k .. k+7] (8 channels of one tap), or of the zero chunk.
 template <int ALOAD>
 PIPNET_DEV const void* a_ptr(const ConvParams& p, const ARow& r, int k) {
-  if (k >= p.Kv) return g_zero_bf;
+  if (k >= p.Kv) return g_zero_bf;   // K padding (packed weights are zero there too)
   if (ALOAD == ALOAD_DENSE) return p.A + r.base + k;
   const int tap = k / p.Cin;
   const int c = k - tap * p.Cin;
@@ -83,19 +82,26 @@ PIPNET_DEV const void* a_ptr(const ConvParams& p, const ARow& r, int k) {
   return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + c;
 }
 
-PIPNET_DEV int swz(int row, int c) { return c ^ ((row >> 1) & 7); }
-
-// Workgroup tile: WGM x WGN waves, each wave TM x TN MFMA 32x32 tiles.
-//   <2,2,2,2> 128x128 (256 threads), <2,2,1,2> 64x128, <2,4,4,2> 256x256 (512 threads).
-template <int WGM_, int WGN_, int TM_, int TN_>
+// Workgroup tile: WGM x WGN waves, each wave TM x TN MFMA 32x32 tiles, BK-deep K tiles in NS
+// LDS stages.  BK = 64: 128-B rows, 8 chunks, chunk ^= (row>>1)&7; BK = 32: 64-B rows, 4
+// chunks, chunk ^= (row>>2)&3 -- either way the 16 lanes of a ds_read_b128 group hit 16
+// distinct 16-B bank slots.
+//   <2,2,2,2,64,2> 128x128, <2,2,1,2,64,2> 64x128, <2,4,4,2,64,2> 256x256 (512 threads),
+//   <2,4,4,2,32,4> 256x256 with 3 K-tiles in flight across the barriers.
+template <int WGM_, int WGN_, int TM_, int TN_, int BK_ = 64, int NS_ = 2>
 struct Cfg {
-  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_;
+  static constexpr int WGM = WGM_, WGN = WGN_, TM = TM_, TN = TN_, BK = BK_, NS = NS_;
   static constexpr int NWAVES = WGM * WGN, NTHREADS = 64 * NWAVES;
   static constexpr int BMT = WGM * 32 * TM, BNT = WGN * 32 * TN;
+  static constexpr int CHUNKS = BK / 8, ROWS_PER_DMA = 64 / CHUNKS;
+  static constexpr int NGROUPS = CHUNKS / 2;            // chunk groups per half-wave per tile
   static constexpr int A_DMA = BMT / ROWS_PER_DMA / NWAVES;
   static constexpr int B_DMA = BNT / ROWS_PER_DMA / NWAVES;
   static constexpr int TILE_ELEMS = (BMT + BNT) * BK;   // bf16 elements of one stage
+  static_assert(BK == 32 || BK == 64, "BK");
+  static_assert(KPAD % BK == 0, "packed K must be a multiple of BK");
   static_assert(A_DMA * ROWS_PER_DMA * NWAVES == BMT && B_DMA * ROWS_PER_DMA * NWAVES == BNT, "DMA split");
+  static PIPNET_DEV int swz(int row, int c) { return BK == 64 ? (c ^ ((row >> 1) & 7)) : (c ^ ((row >> 2) & 3)); }
 };
 
 template <class C>
@@ -107,16 +113,17 @@ using Acc = f32x16[C::TM][C::TN];
 
 template <class C>
 PIPNET_DEV void read_frag(Frag<C>& f, const bf16* buf, int wm, int wn, int lr, int lh, int q) {
-  const int c = lh * 4 + q;
+  constexpr int BK = C::BK;
+  const int c = lh * C::NGROUPS + q;
 #pragma unroll
   for (int i = 0; i < C::TM; ++i) {
     const int ra = wm * 32 * C::TM + i * 32 + lr;
-    f.a[i] = *reinterpret_cast<const bf16x8*>(buf + ra * BK + 8 * swz(ra, c));
+    f.a[i] = *reinterpret_cast<const bf16x8*>(buf + ra * BK + 8 * C::swz(ra, c));
   }
 #pragma unroll
   for (int j = 0; j < C::TN; ++j) {
     const int rb = wn * 32 * C::TN + j * 32 + lr;
-    f.b[j] = *reinterpret_cast<const bf16x8*>(buf + C::BMT * BK + rb * BK + 8 * swz(rb, c));
+    f.b[j] = *reinterpret_cast<const bf16x8*>(buf + C::BMT * BK + rb * BK + 8 * C::swz(rb, c));
   }
 }
 
@@ -132,6 +139,14 @@ PIPNET_DEV void mfma_frag(Acc<C>& acc, const Frag<C>& f) {
 PIPNET_DEV void dma16(const void* src, bf16* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// Retire all but the NPEND youngest vector-memory ops of this wave (LDS-DMA counts as VMEM),
+// drain this wave's LDS reads, then the workgroup barrier -- one asm block, so the LDS-DMA of
+// later tiles stays in flight across it (a __syncthreads() would emit vmcnt(0)).
+template <int NPEND>
+PIPNET_DEV void wait_dma_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(NPEND) : "memory");
 }
 
 PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int bn, int& m0, int& n0) {
@@ -220,12 +235,15 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
   }
 }
 
-// 2 LDS stages, one barrier per 64-deep K tile, fragments software-pipelined over the
-// tile's 4 chunk groups (chunk group q of half-wave h = k 32h + 8q .. +7).
+// NS LDS stages (tile k+NS-1 in flight while tile k is multiplied), one barrier per K tile,
+// fragments software-pipelined over the tile's chunk groups (group q of half-wave h = chunk
+// h*NGROUPS + q = k 8(h*NGROUPS + q) .. +7 of the tile).  NS = 2 waits with vmcnt(0); NS >= 3
+// with a counted vmcnt and a raw s_barrier so younger tiles' DMA spans the barrier.
 template <class C, int EPI, int ALOAD, int MINB>
 __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams p) {
-  constexpr int NS = 2;
+  constexpr int NS = C::NS, BK = C::BK;
   constexpr int NWAVES = C::NWAVES;
+  constexpr int DMA_PER_TILE = C::A_DMA + C::B_DMA;    // per wave
   __shared__ __attribute__((aligned(16))) bf16 smem[NS * C::TILE_ELEMS];
   static_assert(NS * C::TILE_ELEMS * 2 >= NWAVES * 32 * (C::TN * 32 + 4) * 4, "epilogue LDS");
 
@@ -238,30 +256,41 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
   tile_coords(p, C::BMT, C::BNT, m0, n0);
   const int nk = p.K / BK;
 
-  const int drow = lane / CHUNKS;
+  const int drow = lane / C::CHUNKS;
   ARow arow[C::A_DMA];
   int achunk[C::A_DMA];
   const bf16* wsrc[C::B_DMA];
 #pragma unroll
   for (int i = 0; i < C::A_DMA; ++i) {
-    const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
-    achunk[i] = 8 * swz(row, lane % CHUNKS);
+    const int row = (i * NWAVES + wid) * C::ROWS_PER_DMA + drow;
+    achunk[i] = 8 * C::swz(row, lane % C::CHUNKS);
     arow[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
   }
 #pragma unroll
   for (int i = 0; i < C::B_DMA; ++i) {
-    const int row = (i * NWAVES + wid) * ROWS_PER_DMA + drow;
-    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * swz(row, lane % CHUNKS);
+    const int row = (i * NWAVES + wid) * C::ROWS_PER_DMA + drow;
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * C::swz(row, lane % C::CHUNKS);
   }
   auto stage = [&](int kt, int buf) {
     bf16* base = smem + buf * C::TILE_ELEMS;
     const int k0 = kt * BK;
 #pragma unroll
     for (int i = 0; i < C::A_DMA; ++i)
-      dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
+      dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * C::ROWS_PER_DMA * BK);
 #pragma unroll
     for (int i = 0; i < C::B_DMA; ++i)
-      dma16(wsrc[i] + k0, base + C::BMT * BK + (i * NWAVES + wid) * ROWS_PER_DMA * BK);
+      dma16(wsrc[i] + k0, base + C::BMT * BK + (i * NWAVES + wid) * C::ROWS_PER_DMA * BK);
+  };
+  // barrier once tile `need` has landed; `last` = youngest tile whose DMA is in flight
+  auto wait_tile = [&](int need, int last) {
+    if constexpr (NS == 2) {
+      __syncthreads();
+    } else {
+      const int pend = last - need;
+      if (NS >= 4 && pend >= 2) wait_dma_barrier<(NS >= 4 ? 2 : 0) * DMA_PER_TILE>();
+      else if (pend >= 1) wait_dma_barrier<DMA_PER_TILE>();
+      else wait_dma_barrier<0>();
+    }
   };
 
   Acc<C> acc;
@@ -272,24 +301,36 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-  stage(0, 0);
-  __syncthreads();
+  int issued = -1;
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;
+  wait_tile(0, issued);
   Frag<C> fa, fb;
   read_frag<C>(fa, smem, wm, wn, lr, lh, 0);
   int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bf16* buf = smem + cur * C::TILE_ELEMS;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
-    mfma_frag<C>(acc, fa);
-    read_frag<C>(fa, buf, wm, wn, lr, lh, 2);
+    if (kt + NS - 1 < nk) {
+      int nb = cur + NS - 1;
+      if (nb >= NS) nb -= NS;
+      stage(kt + NS - 1, nb);
+      issued = kt + NS - 1;
+    }
+    if constexpr (C::NGROUPS == 4) {
+      read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
+      mfma_frag<C>(acc, fa);
+      read_frag<C>(fa, buf, wm, wn, lr, lh, 2);
+      mfma_frag<C>(acc, fb);
+      read_frag<C>(fb, buf, wm, wn, lr, lh, 3);
+      mfma_frag<C>(acc, fa);
+    } else {
+      read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
+      mfma_frag<C>(acc, fa);
+    }
+    const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
+    wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);     // tile kt+1 landed, tile kt read
+    if (kt + 1 < nk) read_frag<C>(fa, smem + nxt * C::TILE_ELEMS, wm, wn, lr, lh, 0);
     mfma_frag<C>(acc, fb);
-    read_frag<C>(fb, buf, wm, wn, lr, lh, 3);
-    mfma_frag<C>(acc, fa);
-    __syncthreads();                                     // tile kt+1 landed, tile kt read
-    if (kt + 1 < nk) read_frag<C>(fa, smem + (cur ^ 1) * C::TILE_ELEMS, wm, wn, lr, lh, 0);
-    mfma_frag<C>(acc, fb);
-    cur ^= 1;
+    cur = nxt;
   }
   epilogue<EPI, C>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
 }

@@ -100,7 +100,8 @@ int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const v
                             const void* R, int epilogue, void* y, void* stream);
 
 /* Same, with the workgroup tile forced (tuning / tests): tile 0 = 64x128, 1 = 128x128,
- * 2 = 256x256, -1 = automatic (what pipnet_conv2d_nhwc_bf16 uses). */
+ * 2 = 256x256, 3 = 256x256 with 32-deep K tiles in 4 LDS stages, 4 = 128x128 likewise,
+ * -1 = automatic (what pipnet_conv2d_nhwc_bf16 uses). */
 int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
                                  const float* bias, int Cout, int KH, int KW, int stride, int pad,
                                  const void* R, int epilogue, void* y, int tile, void* stream);

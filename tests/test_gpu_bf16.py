@@ -68,7 +68,7 @@ def test_conv2d_nhwc_bf16(gpu, cin, cout, h, k, s, pad, epi):
     _close_bf16(out.cpu(), ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
     (64, 256, 19, 3, 1, 1, _lib.EPI_BIAS_RESID_RELU),   # M = 1083: ragged in every tile size
     (256, 520, 10, 1, 2, 0, _lib.EPI_BIAS),             # N = 520: ragged N tile, strided 1x1

@@ -39,11 +39,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default=None, help="comma-separated layer names")
+    ap.add_argument("--tiles", default="-1,0,1,2,3,4")
     a = ap.parse_args()
     build.build()
     dev = torch.device("cuda:0")
-    total = {t: 0.0 for t in (-1, 0, 1, 2)}
+    tiles = [int(t) for t in a.tiles.split(',')]
+    total = {t: 0.0 for t in tiles}
     for name, h, cin, cout, k, s, pad, epi, cnt in LAYERS:
+        if a.only and name not in a.only.split(","):
+            continue
         x = torch.randn(a.batch, h, h, cin, device=dev).to(torch.bfloat16)
         w = K.pack_conv_weight_bf16(torch.randn(cout, k, k, cin, device=dev) * 0.05)
         b = torch.randn(cout, device=dev)
@@ -51,7 +56,7 @@ def main():
         r = torch.randn(a.batch, oh, oh, cout, device=dev).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
         flops = 2.0 * a.batch * oh * oh * cout * k * k * cin
         line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={K.bf16_conv_tile(a.batch * oh * oh, cout)}"
-        for t in (-1, 0, 1, 2):
+        for t in tiles:
             for _ in range(2):
                 K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=t)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
