@@ -15,7 +15,7 @@ int choose_group_m(int K) {
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 
-using CfgS = Cfg<2, 2, 1, 2>;          //  64 x 128, 256 threads, 48 KiB LDS, 3 workgroups / CU
+using CfgS = Cfg<2, 2, 1, 2, 32, 4>;  //  64 x 128, BK 32 x 4 stages, 48 KiB LDS, 3 workgroups / CU
 using CfgM = Cfg<2, 2, 2, 2>;          // 128 x 128, 256 threads, 64 KiB LDS, 2 workgroups / CU
 using CfgL = Cfg<2, 4, 4, 2>;          // 256 x 256, 512 threads, 128 KiB LDS, 1 workgroup / CU
 using CfgL4 = Cfg<2, 4, 4, 2, 32, 4>;  // 256 x 256, BK 32 x 4 stages (3 tiles in flight), 128 KiB
@@ -24,8 +24,10 @@ using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2
 // Tile choice: the largest tile that still gives every CU at least one workgroup (larger
 // tiles halve the L2 -> LDS bytes per MFMA: 128x128 needs ~64 B/clk/CU at the MFMA rate,
 // the L2's whole bandwidth; 256x256 needs 32), with 32-deep K tiles in 4 stages (+1..+30 %
-// over 64-deep x 2 on the ResNet50 shapes, profiles/r01/conv_bf16_tiles.log).  Mirrored by
-// kernels.py:bf16_conv_tile.
+// over 64-deep x 2 on the ResNet50 shapes, profiles/r01/conv_bf16_tiles.log).  Every tile the
+// automatic choice can pick walks K in the same 32-deep steps, so the MFMA accumulation order
+// -- and therefore every bf16 rounding -- of a pixel does not depend on the batch it is in.
+// Mirrored by kernels.py:bf16_conv_tile.
 int conv_variant(int M, int N) {
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);

@@ -169,13 +169,13 @@ def _chk_bf(t: Tensor, what: str) -> None:
 
 def bf16_conv_tile(m: int, n: int) -> int:
     """Workgroup tile the library picks (mirrors conv_variant in csrc/conv_bf16.hip):
-    0 = 64x128, 3 = 256x256 / 4 = 128x128 (32-deep K tiles, 4 LDS stages)."""
+    0 = 64x128, 3 = 256x256, 4 = 128x128 -- all 32-deep K tiles in 4 LDS stages."""
     if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
         return 3
     return 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
 
 
-_BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 64, 2>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
+_BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
              2: ("pipnet_bf16::Cfg<2, 4, 4, 2, 64, 2>", 1), 3: ("pipnet_bf16::Cfg<2, 4, 4, 2, 32, 4>", 1),
              4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2)}
 
@@ -199,8 +199,8 @@ def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
 def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Optional[Tensor], stride: int,
                      pad: int, epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None, tile: int = -1) -> Tensor:
     """NHWC bf16 implicit-GEMM convolution; w_packed from pack_conv_weight_bf16; bias fp32;
-    tile -1 = automatic, 0/1/2 = forced 64x128 / 128x128 / 256x256 workgroup tile, 3/4 = the
-    256x256 / 128x128 tiles with 32-deep K tiles in 4 LDS stages."""
+    tile -1 = automatic, 0 = 64x128 (32-deep K, 4 stages), 1/2 = 128x128 / 256x256 (64-deep K,
+    2 stages), 3/4 = 256x256 / 128x128 (32-deep K, 4 stages)."""
     _chk_bf(x, "conv input")
     _chk_bf(w_packed, "conv weight")
     if r is not None:

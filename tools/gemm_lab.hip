@@ -10,6 +10,12 @@ static void launch(GemmParams& p, int epi, hipStream_t s) {
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
   if (epi == PIPNET_EPI_BIAS_GELU)
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_BIAS_GELU, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+  else if (epi == EPI_LAB_GELU_PK)
+    hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_PK, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+  else if (epi == EPI_LAB_GELU_PK16)
+    hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_PK16, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+  else if (epi == PIPNET_EPI_BIAS)
+    hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_BIAS, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
   else if (epi == PIPNET_EPI_RESID)
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_RESID, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
   else

@@ -17,6 +17,9 @@ lib.lab_linear.argtypes = [I32, I32, P, I64, P, P, P, P, I64, P, I64, I32, I32, 
 
 VARIANTS = [int(v) for v in os.environ.get("LAB_VARIANTS", "0,1,2,3").split(",")]
 GROUPS = [int(v) for v in os.environ.get("LAB_GROUPS", "1,4,8,16").split(",")]
+# epilogues to run per shape: "native" = the network's own, or EPI codes (A/B the epilogue cost)
+EPIS = os.environ.get("LAB_EPIS", "native").split(",")
+ONLY = os.environ.get("LAB_SHAPES")
 
 
 def shapes(batch=64):
@@ -32,18 +35,21 @@ def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     stream = torch.cuda.current_stream().cuda_stream
-    for name, m, n, k, epi in shapes():
+    for name, m, n, k, epi0 in shapes():
+        if ONLY and name not in ONLY.split(","):
+            continue
         A = torch.randn(m, k, device=dev, generator=g)
         W = torch.randn(n, k, device=dev, generator=g) * 0.05
         b = torch.randn(n, device=dev, generator=g)
         s = torch.randn(n, device=dev, generator=g)
         R = torch.randn(m, n, device=dev, generator=g)
         C = torch.empty(m, n, device=dev)
-        ref = None
+        ref = {}
         times = {}
-        cfgs = list(itertools.product(VARIANTS, GROUPS))
+        epis = [epi0 if e == "native" else int(e) for e in EPIS]
+        cfgs = list(itertools.product(VARIANTS, GROUPS, epis))
         for rnd in range(3):
-            for v, gm in cfgs:
+            for v, gm, epi in cfgs:
                 def run():
                     st = lib.lab_linear(v, gm, A.data_ptr(), k, W.data_ptr(), b.data_ptr(), s.data_ptr(), R.data_ptr(),
                                         n, C.data_ptr(), n, m, n, k, epi, stream)
@@ -55,20 +61,20 @@ def main():
                     run()
                 e1.record()
                 torch.cuda.synchronize()
-                times.setdefault((v, gm), []).append(e0.elapsed_time(e1) / 5 * 1e-3)
+                times.setdefault((v, gm, epi), []).append(e0.elapsed_time(e1) / 5 * 1e-3)
                 if rnd == 0 and v < 10:
-                    if ref is None:
-                        ref = C.clone()
+                    if epi not in ref:
+                        ref[epi] = C.clone()
                     else:
-                        err = (C - ref).abs().max().item()
-                        assert err < 1e-3 * (1 + ref.abs().max().item()), (v, gm, err)
+                        err = (C - ref[epi]).abs().max().item()
+                        assert err < 1e-3 * (1 + ref[epi].abs().max().item()), (v, gm, epi, err)
         f = 2.0 * m * n * k
         line = [f"{name:9s}"]
         best = min(times, key=lambda c: min(times[c]))
         for c in cfgs:
             t = min(times[c])
-            line.append(f"v{c[0]}g{c[1]}:{f / t / 1e12:5.1f}")
-        print(" ".join(line), f"| best v{best[0]} g{best[1]} {f / min(times[best]) / 1e12:.1f} TF", flush=True)
+            line.append(f"v{c[0]}g{c[1]}e{c[2]}:{f / t / 1e12:5.1f}")
+        print(" ".join(line), f"| best v{best[0]} g{best[1]} e{best[2]} {f / min(times[best]) / 1e12:.1f} TF", flush=True)
         del A, W, R, C, ref
 
 
