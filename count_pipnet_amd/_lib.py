@@ -44,6 +44,8 @@ SIGNATURES = {
     "pipnet_count_gumbel_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_count_finish_f32": [P, P, I32, I32, I32, I32, P, P, P],
     "pipnet_count_encode_f32": [P, I32, I32, I32, I32, I32, P, P, P],
+    "pipnet_resize_plan": [P, I32, I32, I32, P, P],
+    "pipnet_resize_normalize_rgb8": [P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P],
 }
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p}
 

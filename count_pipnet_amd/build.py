@@ -33,18 +33,29 @@ def is_stale() -> bool:
     return any(os.path.getmtime(p) > t for p in _deps())
 
 
+def _wait(pr) -> None:
+    proc, src = pr
+    if proc.wait() != 0:
+        raise subprocess.CalledProcessError(proc.returncode, f"hipcc {src}")
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not is_stale():
         return LIB
-    objs = []
-    for src in sources():
+    objs, procs = [], []
+    jobs = max(1, min(int(os.environ.get("MAX_JOBS", "8")), 16))
+    for src in sources():          # one hipcc per translation unit, at most `jobs` at once
         obj = os.path.join(CSRC, os.path.basename(src)[:-4] + ".o")
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-I", os.path.join(REPO, "include")]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        if len(procs) >= jobs:
+            _wait(procs.pop(0))
+        procs.append((subprocess.Popen(cmd), src))
         objs.append(obj)
+    for pr in procs:
+        _wait(pr)
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:

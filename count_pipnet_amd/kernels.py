@@ -376,3 +376,39 @@ def eval_batch(pooled: Tensor, out: Tensor, w: Tensor, ys: Tensor, multiplier: O
               _ptr(multiplier), thr, ys_pred.data_ptr(), score.data_ptr(), cm.data_ptr(), acc.data_ptr(),
               abstained.data_ptr(), ws.data_ptr(), _stream(out))
     return ys_pred, score
+
+
+# ---- evaluation input transform (util/data.py transform_no_augment) ----------------------
+
+def resize_normalize_rgb8(pixels: Tensor, offsets: Tensor, sizes: Tensor, sizes_host, out_hw: Tuple[int, int],
+                          mean, std, grayscale: bool = False, want_u8: bool = False):
+    """Resize(out_hw, BILINEAR) [+ Grayscale(3)] + ToTensor + Normalize of a ragged batch of
+    decoded RGB images packed HWC uint8 on the device (image b at byte offsets[b], shape
+    sizes[b] = (h, w)); ``sizes_host`` is the same [B,2] int32 table on the host.
+    Returns [B,3,oh,ow] fp32 (and the [B,oh,ow,3] uint8 resized image when ``want_u8``)."""
+    import ctypes
+
+    import numpy as np
+    if not (pixels.is_cuda and pixels.dtype == torch.uint8 and pixels.is_contiguous()):
+        raise RuntimeError("resize_normalize_rgb8: pixels must be a contiguous uint8 ROCm device tensor "
+                           "(there is no CPU fallback)")
+    if not (offsets.is_cuda and offsets.dtype == torch.int64 and sizes.is_cuda and sizes.dtype == torch.int32):
+        raise RuntimeError("resize_normalize_rgb8: offsets (int64) / sizes (int32) must be device tensors")
+    sizes_np = np.ascontiguousarray(np.asarray(sizes_host, dtype=np.int32).reshape(-1, 2))
+    b = sizes_np.shape[0]
+    if offsets.shape != (b,) or tuple(sizes.shape) != (b, 2):
+        raise RuntimeError(f"resize_normalize_rgb8: {b} images but offsets {tuple(offsets.shape)}, "
+                           f"sizes {tuple(sizes.shape)}")
+    oh, ow = int(out_hw[0]), int(out_hw[1])
+    kmax, wsb = ctypes.c_int(0), ctypes.c_int64(0)
+    _lib.call("pipnet_resize_plan", sizes_np.ctypes.data, b, oh, ow, ctypes.byref(kmax), ctypes.byref(wsb))
+    dev = pixels.device
+    out = torch.empty((b, 3, oh, ow), device=dev, dtype=torch.float32)
+    out_u8 = torch.empty((b, oh, ow, 3), device=dev, dtype=torch.uint8) if want_u8 else None
+    ws = torch.empty(max(1, wsb.value // 4), device=dev, dtype=torch.int32)
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    _lib.call("pipnet_resize_normalize_rgb8", pixels.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), b, oh, ow,
+              kmax.value, int(bool(grayscale)), m, s, ws.data_ptr(), out.data_ptr(), _ptr(out_u8),
+              torch.cuda.current_stream(dev).cuda_stream)
+    return (out, out_u8) if want_u8 else out

@@ -192,6 +192,27 @@ int pipnet_count_finish_f32(const int32_t* hist, const float* sums, int B, int P
 int pipnet_count_encode_f32(const float* x, int B, int P, int C, int kind, int do_round,
                             const float* w, float* out, void* stream);
 
+/* ---- evaluation input transform ----------------------------------
+ * transform_no_augment of util/data.py (:264-269, :314-321, :500-505, :537-542, :568-574):
+ * Resize((out_h, out_w)) [+ Grayscale(3)] + ToTensor + Normalize(mean, std), applied to a
+ * ragged batch of decoded RGB images (ImageFolder's pil_loader: Image.open().convert('RGB')).
+ * Resize restates Pillow's ImagingResample(BILINEAR) integer arithmetic exactly (torchvision
+ * forwards a PIL image's Resize to it), so the uint8 resized image is bit-identical to
+ * Pillow's and the fp32 output to ToTensor/Normalize of it.
+ *
+ * pipnet_resize_plan (host only): sizes_host [B][2] = (h, w) per image -> kmax (taps per
+ *   output coordinate) and the device workspace size in bytes.
+ * pipnet_resize_normalize_rgb8: pixels = the B images packed HWC uint8 (image b at byte
+ *   offsets[b], device), sizes [B][2] int32 (device), mean3/std3 host float[3], workspace
+ *   (device, from pipnet_resize_plan), out [B,3,out_h,out_w] fp32 NCHW, out_u8 optional
+ *   [B,out_h,out_w,3] uint8 copy of the resized (and grayscaled) image, NULL to skip. */
+int pipnet_resize_plan(const int32_t* sizes_host, int B, int out_h, int out_w, int* kmax,
+                       int64_t* workspace_bytes);
+int pipnet_resize_normalize_rgb8(const uint8_t* pixels, const int64_t* offsets, const int32_t* sizes,
+                                 int B, int out_h, int out_w, int kmax, int grayscale,
+                                 const float* mean3, const float* std3, int32_t* workspace,
+                                 float* out, uint8_t* out_u8, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
