@@ -49,7 +49,27 @@ struct GemmParams {
   int stagger;     // lab: workgroups [stagger_lo, stagger_hi) sleep stagger x s_sleep(127) first
   int stagger_lo, stagger_hi;
   int64_t split_stride;   // split-K (gridDim.y > 1): slab y of C starts at C + y * split_stride
+  long long* stamps;      // lab (ABL & 8): per-workgroup s_memtime stamps + hardware ids
 };
+
+// Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 8
+// int64: start, first K-tile landed, main loop done, epilogue done (s_memtime), HW_ID,
+// XCC_ID, s_memrealtime at start and end.
+template <int ABL>
+PIPNET_DEV void lab_stamp(const GemmParams& p, int slot) {
+  if constexpr ((ABL & 8) != 0) {
+    if (threadIdx.x == 0) {
+      long long* s = p.stamps + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      s[slot] = (long long)__builtin_amdgcn_s_memtime();
+      if (slot == 0) {
+        s[4] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+        s[5] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+        s[6] = (long long)__builtin_amdgcn_s_memrealtime();
+      }
+      if (slot == 3) s[7] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
 
 enum { ALOAD_DENSE = 0, ALOAD_CONV2X2 = 1, ALOAD_CONV = 2 };
 
@@ -362,7 +382,7 @@ PIPNET_DEV void wait_dma_barrier() {
 }
 
 // ABL (tuning-lab ablations only, 0 in the product): 1 = no DMA (stale LDS), 2 = no
-// epilogue (one store per lane keeps the accumulators live), 4 = no barrier.
+// epilogue (one store per lane keeps the accumulators live), 4 = no barrier, 8 = stamps.
 // NS = LDS stages: tile k+NS-1 is in flight while tile k is multiplied.
 template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
@@ -430,10 +450,12 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
 
   Acc acc;
   zero_acc(acc);
+  lab_stamp<ABL>(p, 0);
 
   int issued = -1;                                  // youngest tile whose DMA is in flight
   for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;
   wait_tile(0, issued);
+  lab_stamp<ABL>(p, 1);
   Frag fa, fb;
   read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
   int cur = 0;
@@ -462,6 +484,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     mfma_frag<TM>(acc, fb);
     cur = nxt;
   }
+  lab_stamp<ABL>(p, 2);
   if (ABL & 2) {
     float t = 0.f;
 #pragma unroll
@@ -477,6 +500,10 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     epilogue_vec<EPI, TM>(p, acc, smem, m0, n0, wm, wn, lane, wid);
   else
     epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lr, lh);
+  if constexpr ((ABL & 8) != 0) {
+    __syncthreads();
+    lab_stamp<ABL>(p, 3);
+  }
 }
 
 // ======================================================================================

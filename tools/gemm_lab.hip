@@ -22,6 +22,9 @@ static void launch(GemmParams& p, int epi, hipStream_t s) {
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_NONE, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
 }
 
+static long long* g_stamps = nullptr;
+extern "C" void lab_set_stamps(long long* p) { g_stamps = p; }
+
 extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda, const float* W, const float* bias,
                           const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc, int M, int N, int K,
                           int epi, void* stream) {
@@ -30,13 +33,15 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
   p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
   p.nt = (N + BN - 1) / BN;
   p.group_m = group_m;
-  p.vec_epi = variant >= 20 ? 0 : 1;
-  if (variant >= 20) variant -= 20;
+  const bool scalar_epi = variant >= 20 && variant < 30;   // 2x: variant x with the scalar epilogue
+  p.vec_epi = scalar_epi ? 0 : 1;
+  if (scalar_epi) variant -= 20;
   // group_m >= 100: stagger experiment, group_m = 100*s + g
   p.stagger = group_m / 100;
   p.group_m = group_m % 100;
   p.stagger_lo = 256;
   p.stagger_hi = 512;
+  p.stamps = g_stamps;
   hipStream_t s = (hipStream_t)stream;
   switch (variant) {
     case 0: launch<32, 2, 2, 2>(p, epi, s); break;
@@ -50,6 +55,10 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 10: launch<32, 2, 2, 2, 1>(p, epi, s); break;
     case 11: launch<32, 2, 2, 2, 2>(p, epi, s); break;
     case 13: launch<32, 2, 2, 2, 7>(p, epi, s); break;
+    // stamped (ABL 8) copies of variants 0 / 2 / 3: per-workgroup phase timing
+    case 30: launch<32, 2, 2, 2, 8>(p, epi, s); break;
+    case 32: launch<32, 1, 3, 2, 8>(p, epi, s); break;
+    case 33: launch<16, 2, 2, 3, 8>(p, epi, s); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
