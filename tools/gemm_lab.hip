@@ -51,6 +51,8 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 4: launch<16, 1, 4, 3>(p, epi, s); break;
     case 5: launch<32, 1, 4, 2>(p, epi, s); break;
     case 6: launch<16, 1, 3, 4>(p, epi, s); break;
+    case 7: launch<16, 2, 3, 3>(p, epi, s); break;    // 48 KiB LDS, <=168 VGPRs: 3 workgroups / CU
+    case 8: launch<16, 2, 3, 2>(p, epi, s); break;    // 32 KiB LDS, 3 workgroups / CU
     // ablations of variant 0 (timing only; outputs are wrong)
     case 10: launch<32, 2, 2, 2, 1>(p, epi, s); break;
     case 11: launch<32, 2, 2, 2, 2>(p, epi, s); break;
