@@ -28,7 +28,10 @@ using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2
 // automatic choice can pick walks K in the same 32-deep steps, so the MFMA accumulation order
 // -- and therefore every bf16 rounding -- of a pixel does not depend on the batch it is in.
 // Mirrored by kernels.py:bf16_conv_tile.
-int conv_variant(int M, int N) {
+// N >= 256 layers run the ping-pong 16x16x32 kernel (tile 5) at every batch size -- the
+// choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
+int conv_variant(int M, int N, bool pp_ok) {
+  if (N >= 256 && pp_ok) return 5;
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (N >= 256 && tl >= 256) return 3;
@@ -38,8 +41,28 @@ int conv_variant(int M, int N) {
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
-  if (v < 0) v = conv_variant(p.M, p.N);
-  if (v > 4) return PIPNET_ERR_ARG;
+  const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
+  if (v < 0) v = conv_variant(p.M, p.N, pp_ok);
+  if (v > 5 || (v == 5 && !pp_ok)) return PIPNET_ERR_ARG;
+  if (v == 5) {
+    p.nt = (p.N + 255) / 256;
+    p.mt = (p.M + 255) / 256;
+    p.group_m = choose_group_m(p.K);
+    const dim3 grid(p.mt * p.nt);
+    switch (epi) {
+      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_NONE, ALOAD>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_BIAS, ALOAD>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS_RELU:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_BIAS_RELU, ALOAD>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_BIAS_RESID_RELU:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_BIAS_RESID_RELU, ALOAD>), grid, dim3(512), 0, s, p);
+        break;
+      default: return PIPNET_ERR_ARG;
+    }
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   const int bm = (v == 2 || v == 3) ? 256 : (v == 0 ? 64 : 128), bn = (v == 2 || v == 3) ? 256 : 128;
   p.nt = (p.N + bn - 1) / bn;
   p.mt = (p.M + bm - 1) / bm;

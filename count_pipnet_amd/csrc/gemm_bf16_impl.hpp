@@ -335,4 +335,237 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
   epilogue<EPI, C>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
 }
 
+// ======================================================================================
+// Ping-pong 256x256 tile on v_mfma_f32_16x16x32_bf16 (cdna_hip_programming.md "256^2
+// 8-phase template" structure, re-derived for 32-deep K tiles in 4 LDS stages).
+//
+// 8 waves = 2 groups (wr = wid >> 2) x 4 column blocks (wc); wave (wr, wc) owns the 128x64
+// output block rows wr*128.., cols wc*64.. as 8 x 4 MFMA 16x16 tiles.  A K-tile (32 deep, one
+// MFMA k-step) is two PHASES of 16 MFMAs (row half 0 / 1 of the wave's block), each phase
+//     [ds_read fragments of this phase] [LDS-DMA] s_barrier | MFMA x16 (prio 1) | s_barrier
+// and group 1 runs one barrier behind group 0 (one extra s_barrier before the loop), so on
+// every SIMD one wave's MFMA segment coincides with its partner's read / DMA / barrier
+// segment and the matrix pipe alternates between the two instead of both stalling together.
+//
+// LDS: 4 stages x (256 A rows + 256 B rows) x 64 B.  K-tile t+3 is fetched (4 x 1 KiB
+// pieces per wave) at the top of phase 1 of K-tile t into the stage of K-tile t-1: every
+// wave retired its reads of t-1 (compiler lgkmcnt before the MFMAs of the phase that read
+// them) before the barrier the DMA issue follows, for both groups (derivation in DESIGN.md).
+// Each wave waits for its own pieces of K-tile t+1 (vmcnt counting the 4 or 8 younger
+// pieces) before the first barrier of phase 1 of K-tile t; group 0 reads t+1 after its next
+// barrier, group 1 one barrier later -- both after every wave's wait.
+//
+// Rows are 64 B (4 x 16-B chunks); chunk c of row r lives at physical chunk c ^ g(r),
+// g(r) = (-(r >> 2)) & 3: with the 16x16x32 operand map (lane l reads row l & 15, chunk
+// l >> 4) every ds_read_b128 lane group of 16 hits 16 distinct 16-B bank slots.  The DMA
+// writes lane-linear, so the swizzle is applied to its source address.
+// Requirements: Cin % 32 == 0 (a K-tile never straddles two taps), N % 8 == 0, K % 32 == 0.
+// ======================================================================================
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+namespace pp {
+constexpr int BM = 256, BN = 256, BK = 32, NS = 4, NT = 512;
+constexpr int ROWB = BK * 2;                          // 64 B per LDS row
+constexpr int STAGE_BYTES = (BM + BN) * ROWB;         // 32 KiB
+constexpr int EPI_LD = 68;                            // fp32 epilogue rows: 64 + 4 pad
+constexpr int EPI_BYTES = 8 * 64 * EPI_LD * 4;        // 8 waves x 64 rows
+constexpr int SMEM_BYTES = NS * STAGE_BYTES > EPI_BYTES ? NS * STAGE_BYTES : EPI_BYTES;
+PIPNET_DEV int g(int r) { return (-(r >> 2)) & 3; }
+}  // namespace pp
+
+template <int NPEND>
+PIPNET_DEV void pp_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPEND) : "memory");
+}
+PIPNET_DEV void pp_barrier() {
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI, int ALOAD>
+__global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
+  using namespace pp;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  tile_coords(p, BM, BN, m0, n0);
+  const int nk = p.K / BK;
+
+  // ---- DMA sources: pieces wid and wid + 8 of A and of B (16 rows x 64 B each) ----
+  const int drow = lane >> 2;                                  // row within a piece
+  const int dchunk = 8 * ((lane & 3) ^ g(drow));               // logical chunk (elements)
+  ARow ar[2];
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (wid + 8 * i) + drow;
+    ar[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
+  }
+  // (tap, channel) of the K-tile the DMA fetches next, advanced incrementally (a 32-deep
+  // K-tile never straddles a tap: Cin % 32 == 0), so no division in the loop.
+  int d_c = 0, d_kx = 0, d_ky = 0;
+  auto a_src = [&](const ARow& r, int k0) -> const void* {
+    if (k0 >= p.Kv) return g_zero_bf;
+    if (ALOAD == ALOAD_DENSE) return p.A + r.base + k0 + dchunk;
+    const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
+    if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
+    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + d_c + dchunk;
+  };
+  auto advance = [&]() {
+    if (ALOAD != ALOAD_DENSE) {
+      d_c += BK;
+      if (d_c == p.Cin) {
+        d_c = 0;
+        if (++d_kx == p.KW) d_kx = 0, ++d_ky;
+      }
+    }
+  };
+  auto stage = [&](int kt) {                                   // 4 x 1 KiB pieces of this wave, in order
+    unsigned char* base = smem + (kt & (NS - 1)) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a_src(ar[i], kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + BM * ROWB +
+                                                                                 (wid + 8 * i) * 1024),
+                                       16, 0, 0);
+    advance();
+  };
+
+  // ---- fragment reads: lane reads row (l & 15) of a 16-row block, logical chunk l >> 4 ----
+  const int fr = lane & 15;
+  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));     // byte offset inside a 16-row block
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
+  };
+  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 64 + n * 16) * ROWB + fofs);
+  };
+
+  f32x4v acc[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: K-tiles 0..2 in flight, wait for tile 0 (8 younger pieces at most)
+  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0);
+  if (nk >= 3) pp_wait_vm<8>();
+  else if (nk == 2) pp_wait_vm<4>();
+  else pp_wait_vm<0>();
+  pp_barrier();
+  if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
+
+  bf16x8v fa[4], fb[4];
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = smem + (kt & (NS - 1)) * STAGE_BYTES;
+    // ---- phase 0: rows 0..63 of the wave's block ----
+    read_b(fb, st);
+    read_a(fa, st, 0);
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    // ---- phase 1: rows 64..127; fetch K-tile kt+3 (DMA first: an M0 write for the DMA
+    // would otherwise wait for this phase's fragment reads); wait for K-tile kt+1 ----
+    if (kt + 3 < nk) stage(kt + 3);
+    read_a(fa, st, 1);
+    const int younger = (kt + 3 < nk ? kt + 3 : nk - 1) - (kt + 1);   // tiles issued after kt+1
+    if (younger >= 2) pp_wait_vm<8>();
+    else if (younger == 1) pp_wait_vm<4>();
+    else pp_wait_vm<0>();
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+  }
+  if (wr == 0) pp_barrier();                                   // re-align the groups
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pp_barrier();                                                // stage buffers free for the epilogue
+
+  // ---- epilogue: per row half, fp32 re-layout in the wave's own LDS rows, then 8 channels per lane ----
+  constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
+  float* wt = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
+  const int c8 = lane & 7;
+  const int n = n0 + wc * 64 + 8 * c8;
+  const bool nok = n < p.N;
+  f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
+    b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
+    b1 = *reinterpret_cast<const f32x4v*>(p.bias + n + 4);
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    bf16x8v rr[8];
+    if (HAS_R) {
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int m = min(m0 + wr * 128 + half * 64 + it * 8 + (lane >> 3), p.M - 1);
+        if (nok) rr[it] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          wt[(r * 16 + 4 * (lane >> 4) + i) * EPI_LD + nn * 16 + fr] = acc[half * 4 + r][nn][i];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int row = it * 8 + (lane >> 3);
+      const int m = m0 + wr * 128 + half * 64 + row;
+      f32x4v x0 = *reinterpret_cast<const f32x4v*>(wt + row * EPI_LD + 8 * c8);
+      f32x4v x1 = *reinterpret_cast<const f32x4v*>(wt + row * EPI_LD + 8 * c8 + 4);
+      x0 += b0;
+      x1 += b1;
+      if (HAS_R) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] += (float)rr[it][e];
+          x1[e] += (float)rr[it][4 + e];
+        }
+      }
+      if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          x0[e] = fmaxf(x0[e], 0.f);
+          x1[e] = fmaxf(x1[e], 0.f);
+        }
+      }
+      bf16x8v o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (bf16)x0[e];
+        o[4 + e] = (bf16)x1[e];
+      }
+      if (m < p.M && nok) *reinterpret_cast<bf16x8v*>(p.C + (int64_t)m * p.ldc + n) = o;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // reads done before the next half's writes
+  }
+}
+
 }  // namespace pipnet_bf16

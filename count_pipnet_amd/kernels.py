@@ -167,9 +167,12 @@ def _chk_bf(t: Tensor, what: str) -> None:
         raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
 
 
-def bf16_conv_tile(m: int, n: int) -> int:
+def bf16_conv_tile(m: int, n: int, pp_ok: bool = True) -> int:
     """Workgroup tile the library picks (mirrors conv_variant in csrc/conv_bf16.hip):
-    0 = 64x128, 3 = 256x256, 4 = 128x128 -- all 32-deep K tiles in 4 LDS stages."""
+    5 = 256x256 ping-pong on 16x16x32 MFMAs (every N >= 256 layer with Cin % 32 == 0, any M),
+    else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all 32-deep K tiles in 4 LDS stages."""
+    if n >= 256 and pp_ok:
+        return 5
     if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
         return 3
     return 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
@@ -180,9 +183,12 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
              4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2)}
 
 
-def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1) -> str:
+def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True) -> str:
     """rocprof name of the bf16 conv instantiation."""
-    cfg, minb = _BF16_CFG[bf16_conv_tile(m, n) if tile < 0 else tile]
+    t = bf16_conv_tile(m, n, pp_ok) if tile < 0 else tile
+    if t == 5:
+        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}>"
+    cfg, minb = _BF16_CFG[t]
     return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}>"
 
 
@@ -216,7 +222,8 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     y = torch.empty((b, oh, ow, cout), device=x.device, dtype=torch.bfloat16)
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile), 2.0 * m * cout * k,
+    pp_ok = (aload == 0 or cin % 32 == 0) and kp % 32 == 0
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok), 2.0 * m * cout * k,
             lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
                               _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), tile,
                               _stream(x)))

@@ -68,19 +68,23 @@ def test_conv2d_nhwc_bf16(gpu, cin, cout, h, k, s, pad, epi):
     _close_bf16(out.cpu(), ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
     (64, 256, 19, 3, 1, 1, _lib.EPI_BIAS_RESID_RELU),   # M = 1083: ragged in every tile size
     (256, 520, 10, 1, 2, 0, _lib.EPI_BIAS),             # N = 520: ragged N tile, strided 1x1
+    (96, 264, 21, 1, 1, 0, _lib.EPI_BIAS_RELU),         # dense 1x1, K = 96 -> 128 padded (K tail of zeros)
+    (512, 512, 12, 3, 1, 1, _lib.EPI_BIAS_RELU),        # layer4 3x3: 144 K-tiles, padding taps
 ])
 def test_conv2d_nhwc_bf16_every_tile(gpu, tile, cin, cout, h, k, s, pad, epi):
-    """Each workgroup tile (64x128, 128x128, 256x256) forced on ragged shapes."""
+    """Each workgroup tile (64x128, 128x128, 256x256, ping-pong 256x256) forced on ragged shapes."""
     g = torch.Generator().manual_seed(tile * 11 + cout)
     x = _bf(torch.randn(3, cin, h, h, generator=g))
     w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
     b = torch.randn(cout, generator=g).double()
     y = F.conv2d(x, _bf(w), b, stride=s, padding=pad)
     r = _bf(torch.randn(*y.shape, generator=g))
+    if epi == _lib.EPI_BIAS_RELU:
+        y = torch.relu(y)
     if epi == _lib.EPI_BIAS_RESID_RELU:
         y = torch.relu(y + r)
     ref = _bf(y.float()).permute(0, 2, 3, 1)
@@ -99,6 +103,18 @@ def test_conv_bf16_layout_asymmetric(gpu):
     w = ((torch.arange(n * n) % 251) / 8.0).view(n, n)              # multiples of 1/8 < 32: exact in bf16
     out = K.conv2d_nhwc_bf16(x.contiguous().to(torch.bfloat16).to(gpu),
                              K.pack_conv_weight_bf16(w.view(n, 1, 1, n).to(gpu)), 1, 1, None, 1, 0, _lib.EPI_NONE)
+    assert torch.equal(out.float().cpu().view(n, n), w.t().contiguous())
+
+
+@pytest.mark.parametrize("n", [256, 320])
+def test_conv_bf16_pp_layout_asymmetric(gpu, n):
+    """The ping-pong tile (16x16x32 operand map, 64-B swizzled rows, per-wave epilogue
+    re-layout) on an identity input: out[i] = column i of an asymmetric exact weight."""
+    x = torch.eye(n).view(1, n, 1, n)
+    w = ((torch.arange(n * n) % 253) / 8.0).view(n, n)
+    out = K.conv2d_nhwc_bf16(x.contiguous().to(torch.bfloat16).to(gpu),
+                             K.pack_conv_weight_bf16(w.view(n, 1, 1, n).to(gpu)), 1, 1, None, 1, 0, _lib.EPI_NONE,
+                             tile=5)
     assert torch.equal(out.float().cpu().view(n, n), w.t().contiguous())
 
 
