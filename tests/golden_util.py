@@ -14,8 +14,10 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def golden_names():
-    """Forward golden cases (eval_* fixtures belong to the eval_pipnet metric loop)."""
-    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz") and not f.startswith("eval_"))
+    """Forward golden cases (eval_* fixtures belong to the eval_pipnet metric loop, input_*
+    to the input transform, tests/test_input_oracle.py)."""
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR)
+                  if f.endswith(".npz") and not f.startswith(("eval_", "input_")))
 
 
 def eval_golden_names():
