@@ -42,6 +42,7 @@ SIGNATURES = {
     "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],
     "pipnet_nonneg_linear_f32": [P, I32, I32, P, P, I32, I32, F32, P, P, P],
     "pipnet_count_gumbel_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
+    "pipnet_count_gumbel_devseed_f32": [P, I32, I32, I32, F32, P, P, P, P],
     "pipnet_count_finish_f32": [P, P, I32, I32, I32, I32, P, P, P],
     "pipnet_count_encode_f32": [P, I32, I32, I32, I32, I32, P, P, P],
     "pipnet_resize_plan": [P, I32, I32, I32, P, P],

@@ -74,8 +74,14 @@ class CountPIPNet(nn.Module):
             noise = act.exp_noise
             if noise is not None:
                 noise = noise.to(device=logits.device, dtype=torch.float32).contiguous()
-            seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())   # fresh noise per call
-            proto, hist = K.count_gumbel(logits, act.tau, noise, seed)
+                proto, hist = K.count_gumbel(logits, act.tau, noise, 0)
+            elif torch.cuda.is_current_stream_capturing():
+                # HIP-graph capture: the key must live in device memory so that every replay
+                # draws fresh noise (count_pipnet_amd.graph)
+                proto, hist = K.count_gumbel_devseed(logits, act.tau, self._graph_seed_state(logits.device))
+            else:
+                seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())   # fresh noise per call
+                proto, hist = K.count_gumbel(logits, act.tau, None, seed)
             counts, clamped = K.count_finish(hist, None, self._max_count, do_round)
         else:
             logits = add_on_logits_hip(self._add_on, feats, activation=nn.Softmax)
@@ -85,6 +91,14 @@ class CountPIPNet(nn.Module):
         cls = self._classification
         _, out = K.nonneg_linear(inter, cls.weight, cls.bias, None)
         return nhwc_as_nchw(proto), (clamped if inference else counts), out
+
+    def _graph_seed_state(self, device):
+        st = getattr(self, "_hip_seed_state", None)
+        if st is None or st.device != device:
+            seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+            st = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+            self._hip_seed_state = st           # plain attribute: not a parameter / buffer
+        return st
 
     def _calculate_counts_for_testing(self, proto_features):
         return proto_features.sum(dim=(2, 3))

@@ -10,6 +10,21 @@
 #include "common.hpp"
 
 namespace {
+// Zero-fill by a kernel rather than a memset call: the launch is captured as an ordinary
+// kernel node when the stream is being recorded into a HIP graph (count_pipnet_amd.graph); a
+// memset issued during capture was observed NOT to take effect on replay.
+__global__ __launch_bounds__(256) void zero_u32_kernel(uint32_t* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+}
+inline bool zero_fill(void* p, int64_t n_u32, hipStream_t s) {
+  const int64_t blocks = (n_u32 + 255) / 256 < 1024 ? (n_u32 + 255) / 256 : 1024;
+  hipLaunchKernelGGL(zero_u32_kernel, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, s,
+                     reinterpret_cast<uint32_t*>(p), n_u32);
+  return hipGetLastError() == hipSuccess;
+}
+}  // namespace
+
+namespace {
 
 constexpr int HEAD_THREADS = 256;
 constexpr int PIX_PER_BLOCK = 32;
@@ -236,8 +251,10 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
                                                                     float inv_tau,
                                                                     const float* __restrict__ exp_noise,
                                                                     uint64_t seed, uint64_t offset,
+                                                                    const uint64_t* __restrict__ seed_dev,
                                                                     float* __restrict__ proto,
                                                                     int32_t* __restrict__ hist) {
+  if (seed_dev) seed = *seed_dev;     // graph-replay form: the seed lives in device memory
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int pix0 = blockIdx.x * PIX_PER_BLOCK;
@@ -345,7 +362,7 @@ int softmax_pool_launch(const T* feat, int B, int HW, int P, int pool_mode, floa
   const int nj = nj_bucket(P);
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(pooled, 0, sizeof(float) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  if (!zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
 #define SP_CALL(N)                                                                                          \
   if (pool_mode == 0)                                                                                       \
@@ -371,7 +388,7 @@ extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, 
   if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1) || !pooled) return PIPNET_ERR_ARG;
   if (B == 0) return PIPNET_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(pooled, 0, sizeof(float) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  if (!zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
 #define SPV_CALL(N)                                                                                            \
   if (pool_mode == 0)                                                                                          \
@@ -402,23 +419,47 @@ extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const floa
   return PIPNET_OK;
 }
 
-extern "C" int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau, const float* exp_noise,
-                                       uint64_t seed, uint64_t offset, float* proto, int32_t* hist, void* stream) {
+namespace {
+int count_gumbel_launch(const float* logits, int B, int HW, int P, float tau, const float* exp_noise, uint64_t seed,
+                        uint64_t offset, const uint64_t* seed_dev, float* proto, int32_t* hist, void* stream) {
   if (B < 0 || HW <= 0 || P <= 0 || !(tau > 0.f) || !logits || !proto || !hist) return PIPNET_ERR_ARG;
   if (B == 0) return PIPNET_OK;
   const int nj = nj_bucket(P);
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (hipMemsetAsync(hist, 0, sizeof(int32_t) * (size_t)B * P, s) != hipSuccess) return PIPNET_ERR_HIP;
+  if (!zero_fill(hist, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
   const float inv_tau = 1.0f / tau;
 #define CG_CALL(N)                                                                                              \
   hipLaunchKernelGGL((count_gumbel_kernel<N>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, exp_noise, \
-                     seed, offset, proto, hist);
+                     seed, offset, seed_dev, proto, hist);
   PIPNET_NJ_SWITCH(nj, CG_CALL)
 #undef CG_CALL
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
+}
+
+// splitmix64 step of the device-resident Philox key (one thread).
+__global__ void seed_advance_kernel(uint64_t* seed) {
+  uint64_t z = (*seed += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  seed[1] = z ^ (z >> 31);
+}
+}  // namespace
+
+extern "C" int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau, const float* exp_noise,
+                                       uint64_t seed, uint64_t offset, float* proto, int32_t* hist, void* stream) {
+  return count_gumbel_launch(logits, B, HW, P, tau, exp_noise, seed, offset, nullptr, proto, hist, stream);
+}
+
+extern "C" int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int HW, int P, float tau,
+                                               uint64_t* seed_state, float* proto, int32_t* hist, void* stream) {
+  if (!seed_state) return PIPNET_ERR_ARG;
+  if (B <= 0) return count_gumbel_launch(logits, B, HW, P, tau, nullptr, 0, 0, seed_state + 1, proto, hist, stream);
+  hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, seed_state);
+  PIPNET_CHECK_LAUNCH();
+  return count_gumbel_launch(logits, B, HW, P, tau, nullptr, 0, 0, seed_state + 1, proto, hist, stream);
 }
 
 extern "C" int pipnet_count_finish_f32(const int32_t* hist, const float* sums, int B, int P, int max_count,

@@ -330,6 +330,20 @@ def count_gumbel(logits_nhwc: Tensor, tau: float, exp_noise_nchw: Optional[Tenso
     return proto, hist
 
 
+def count_gumbel_devseed(logits_nhwc: Tensor, tau: float, seed_state: Tensor) -> Tuple[Tensor, Tensor]:
+    """count_gumbel with the Philox key in device memory (seed_state: int64[2] on the device),
+    advanced on the stream per call -- the form a captured HIP graph replays."""
+    _chk(logits_nhwc, "prototype logits")
+    if not (seed_state.is_cuda and seed_state.dtype == torch.int64 and seed_state.numel() == 2):
+        raise RuntimeError("count_gumbel_devseed: seed_state must be a 2-element int64 device tensor")
+    b, h, w, p = logits_nhwc.shape
+    proto = torch.empty_like(logits_nhwc)
+    hist = torch.empty((b, p), device=logits_nhwc.device, dtype=torch.int32)
+    _lib.call("pipnet_count_gumbel_devseed_f32", logits_nhwc.data_ptr(), b, h * w, p, float(tau),
+              seed_state.data_ptr(), proto.data_ptr(), hist.data_ptr(), _stream(logits_nhwc))
+    return proto, hist
+
+
 def count_finish(hist: Optional[Tensor], sums: Optional[Tensor], max_count: int, do_round: bool) -> Tuple[Tensor, Tensor]:
     ref = hist if hist is not None else sums
     b, p = ref.shape

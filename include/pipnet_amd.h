@@ -181,6 +181,13 @@ int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau
                             const float* exp_noise, uint64_t seed, uint64_t offset, float* proto,
                             int32_t* hist, void* stream);
 
+/* Same, graph-replayable: the Philox key is device memory.  seed_state: uint64[2] on the
+ * device ([0] a splitmix64 counter, [1] the key); each call first advances the counter and
+ * derives a new key on the stream (fresh noise per call, as the reference draws fresh
+ * noise), so a captured hipGraph replays with new noise every time. */
+int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int HW, int P, float tau,
+                                    uint64_t* seed_state, float* proto, int32_t* hist, void* stream);
+
 /* Count finish (count_pipnet.py:88-97): counts_raw = float(hist) (or sums when hist is
  * NULL), clamped = clamp(round?(counts), 0, max_count) -- round when do_round.
  * sums: [B,P] float (softmax activation path) used when hist == NULL. */

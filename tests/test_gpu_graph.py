@@ -1,0 +1,66 @@
+"""HIP-graph replay of the inference forward (count_pipnet_amd.graph.GraphedForward) equals
+the eager HIP forward bit for bit, follows in-place classifier updates, and draws fresh
+Gumbel noise per replay."""
+import pytest
+import torch
+
+from golden_util import golden_inputs, load_golden
+from model_util import build_model
+
+pytestmark = pytest.mark.gpu
+
+
+def _net(name, gpu):
+    meta, rec = load_golden(name)
+    return build_model(meta).to(gpu), golden_inputs(meta).to(gpu), meta
+
+
+@pytest.mark.parametrize("name", ["c2_pipnet_convnext26", "pipnet_mid_addon", "c3_pipnet_resnet50"])
+def test_graph_replay_equals_eager(gpu, name):
+    from count_pipnet_amd.graph import GraphedForward
+    net, xs, _ = _net(name, gpu)
+    with torch.no_grad():
+        ref = [t.clone() for t in net(xs, inference=True)]
+    g = GraphedForward(net)
+    for _ in range(2):
+        outs = g(xs)
+        torch.cuda.synchronize()
+        for a, b in zip(outs, ref):
+            assert torch.equal(a, b)
+    # in-place classifier update (eval_pipnet sparsification) is seen by the replay
+    with torch.no_grad():
+        net._classification.weight.mul_(0.5)
+        ref2 = net(xs, inference=True)[2].clone()
+    out2 = g(xs)[2]
+    torch.cuda.synchronize()
+    assert torch.equal(out2, ref2)
+
+
+def test_graph_count_injected_noise_equals_eager(gpu):
+    from count_pipnet_amd.graph import GraphedForward
+    from count_pipnet_amd.synthetic import synth_exponential
+    net, xs, meta = _net("c1_count_identity", gpu)
+    b, p = xs.shape[0], net._num_prototypes
+    act = list(net._add_on)[-1]
+    act.exp_noise = synth_exponential((b, p, 8, 8), seed=5).to(gpu)
+    with torch.no_grad():
+        ref = [t.clone() for t in net(xs, inference=True)]
+    outs = GraphedForward(net)(xs)
+    torch.cuda.synchronize()
+    for a, r in zip(outs, ref):
+        assert torch.equal(a, r)
+
+
+def test_graph_count_fresh_noise_per_replay(gpu):
+    from count_pipnet_amd.graph import GraphedForward
+    net, xs, meta = _net("c1_count_identity", gpu)
+    list(net._add_on)[-1].exp_noise = None
+    g = GraphedForward(net)
+    p1 = g(xs)[0].clone()
+    p2 = g(xs)[0].clone()
+    torch.cuda.synchronize()
+    assert not torch.equal(p1, p2)                       # new Philox key per replay
+    for p in (p1, p2):                                   # still hard one-hot maps
+        s = p.sum(dim=1)
+        assert torch.allclose(s, torch.ones_like(s))
+        assert torch.equal((p > 0).sum(dim=1), torch.ones_like(s, dtype=torch.int64))

@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--graph", action="store_true", help="also time HIP-graph replay (count_pipnet_amd.graph)")
     a = ap.parse_args()
     build.build()
     dev = torch.device("cuda:0")
@@ -78,9 +79,24 @@ def main():
         ips = cfg["batch"] * a.steps / el
         dt = cfg["args"].get("hip_dtype", "f32")
         peak = 2500.0 if dt == "bf16" else 157.3
-        print(json.dumps(dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
-                              image_size=cfg["size"], dtype=dt, model_tflops=ips * cfg["gflop"] / 1e3,
-                              model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak)), flush=True)
+        rec = dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
+                   image_size=cfg["size"], dtype=dt, model_tflops=ips * cfg["gflop"] / 1e3,
+                   model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak)
+        if a.graph:
+            from count_pipnet_amd.graph import GraphedForward
+            g = GraphedForward(net)
+            for _ in range(a.warmup):
+                g(xs)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                g(xs)
+            torch.cuda.synchronize()
+            elg = time.perf_counter() - t0
+            rec["graph_images_per_sec"] = cfg["batch"] * a.steps / elg
+            rec["graph_ms_per_step"] = elg / a.steps * 1e3
+            del g
+        print(json.dumps(rec), flush=True)
         del net, xs
         torch.cuda.empty_cache()
 
