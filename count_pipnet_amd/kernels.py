@@ -247,12 +247,25 @@ def nchw_to_nhwc_bf16(x: Tensor, cpad: int) -> Tensor:
     return y
 
 
-def softmax_pool_bf16(feat_nhwc: Tensor, pool_mode: int) -> Tuple[Tensor, Tensor]:
+def _head_out(out, b, h, w, p, dev):
+    """Caller-provided (proto [B,h,w,P], pooled [B,P]) fp32 contiguous outputs, or new ones."""
+    if out is None:
+        return (torch.empty((b, h, w, p), device=dev, dtype=torch.float32),
+                torch.empty((b, p), device=dev, dtype=torch.float32))
+    proto, pooled = out
+    if tuple(proto.shape) != (b, h, w, p) or tuple(pooled.shape) != (b, p):
+        raise RuntimeError(f"softmax_pool: out shapes {tuple(proto.shape)}, {tuple(pooled.shape)} do not match "
+                           f"{(b, h, w, p)}, {(b, p)}")
+    _chk(proto, "proto out")
+    _chk(pooled, "pooled out")
+    return proto, pooled
+
+
+def softmax_pool_bf16(feat_nhwc: Tensor, pool_mode: int, out=None) -> Tuple[Tensor, Tensor]:
     """bf16 logits [B,h,w,P] -> fp32 (proto [B,h,w,P], pooled [B,P])."""
     _chk_bf(feat_nhwc, "prototype logits")
     b, h, w, p = feat_nhwc.shape
-    proto = torch.empty((b, h, w, p), device=feat_nhwc.device, dtype=torch.float32)
-    pooled = torch.empty((b, p), device=feat_nhwc.device, dtype=torch.float32)
+    proto, pooled = _head_out(out, b, h, w, p, feat_nhwc.device)
     _lib.call("pipnet_softmax_pool_bf16", feat_nhwc.data_ptr(), b, h * w, p, pool_mode, proto.data_ptr(),
               pooled.data_ptr(), _stream(feat_nhwc))
     return proto, pooled
@@ -288,25 +301,34 @@ def layernorm(x: Tensor, w: Tensor, b: Tensor, out: Optional[Tensor] = None) -> 
     return y
 
 
-def softmax_pool(feat_nhwc: Tensor, pool_mode: int) -> Tuple[Tensor, Tensor]:
-    """feat [B,h,w,P] -> (proto [B,h,w,P], pooled [B,P]); pool 0 = max, 1 = sum."""
+def softmax_pool(feat_nhwc: Tensor, pool_mode: int, out=None) -> Tuple[Tensor, Tensor]:
+    """feat [B,h,w,P] -> (proto [B,h,w,P], pooled [B,P]); pool 0 = max, 1 = sum.
+    ``out`` = (proto, pooled) to write into (e.g. batch slices of a larger output)."""
     _chk(feat_nhwc, "prototype logits")
     b, h, w, p = feat_nhwc.shape
-    proto = torch.empty_like(feat_nhwc)
-    pooled = torch.empty((b, p), device=feat_nhwc.device, dtype=torch.float32)
+    proto, pooled = _head_out(out, b, h, w, p, feat_nhwc.device)
     _lib.call("pipnet_softmax_pool_f32", feat_nhwc.data_ptr(), b, h * w, p, pool_mode, proto.data_ptr(),
               pooled.data_ptr(), _stream(feat_nhwc))
     return proto, pooled
 
 
-def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float]) -> Tuple[Tensor, Tensor]:
-    """(x', out) with x' = where(x < thresh, 0, x) (or x) and out = x' relu(w)^T + bias."""
+def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float],
+                  out=None) -> Tuple[Tensor, Tensor]:
+    """(x', out) with x' = where(x < thresh, 0, x) (or x) and out = x' relu(w)^T + bias.
+    ``out`` = (x', logits) to write into."""
     _chk(x, "classifier input")
     _chk(w, "classifier weight")
     b, d = x.shape
     k = w.shape[0]
-    x_out = torch.empty_like(x)
-    out = torch.empty((b, k), device=x.device, dtype=torch.float32)
+    if out is None:
+        x_out = torch.empty_like(x)
+        out = torch.empty((b, k), device=x.device, dtype=torch.float32)
+    else:
+        x_out, out = out
+        if tuple(x_out.shape) != (b, d) or tuple(out.shape) != (b, k):
+            raise RuntimeError("nonneg_linear: out shapes do not match")
+        _chk(x_out, "classifier input out")
+        _chk(out, "logits out")
     _lib.call("pipnet_nonneg_linear_f32", x.data_ptr(), b, d, w.data_ptr(), _ptr(bias), k,
               0 if thresh is None else 1, 0.0 if thresh is None else float(thresh), x_out.data_ptr(),
               out.data_ptr(), _stream(x))

@@ -64,3 +64,29 @@ def test_graph_count_fresh_noise_per_replay(gpu):
         s = p.sum(dim=1)
         assert torch.allclose(s, torch.ones_like(s))
         assert torch.equal((p > 0).sum(dim=1), torch.ones_like(s, dtype=torch.int64))
+
+
+def test_stream_split_bit_identical_and_graph(gpu):
+    """Opt-in stream split: a batch >= 32 runs as concurrent sub-batches on 2 (3) streams,
+    outputs bit-identical to the one-stream forward, also under HIP-graph capture."""
+    from count_pipnet_amd.graph import GraphedForward
+    from count_pipnet_amd.pipnet import set_stream_split, stream_split
+    from count_pipnet_amd.synthetic import synth_images
+    net, _, _ = _net("pipnet_mid_addon", gpu)
+    xs = synth_images(40, 64, seed=9).to(gpu)
+    assert stream_split(net, xs) == 1                    # off by default
+    set_stream_split(net, 2)
+    assert stream_split(net, xs) == 2
+    with torch.no_grad():
+        split = [t.clone() for t in net(xs, inference=True)]
+        set_stream_split(net, 1)
+        one = [t.clone() for t in net(xs, inference=True)]
+        set_stream_split(net, 3)
+        three = [t.clone() for t in net(xs, inference=True)]
+    for a, b, c in zip(split, one, three):
+        assert torch.equal(a, b) and torch.equal(c, b)
+    set_stream_split(net, 2)
+    outs = GraphedForward(net)(xs)
+    torch.cuda.synchronize()
+    for a, b in zip(outs, one):
+        assert torch.equal(a, b)
