@@ -40,8 +40,22 @@ def _wait(pr) -> None:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile if stale.  Concurrent callers (one process per GPU under torchrun) serialise on
+    a file lock and re-check staleness, so only the first one compiles."""
     if not force and not is_stale():
         return LIB
+    import fcntl
+    with open(os.path.join(PKG, ".build.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            if not force and not is_stale():
+                return LIB
+            return _build_locked(verbose)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
+
+
+def _build_locked(verbose: bool) -> str:
     objs, procs = [], []
     jobs = max(1, min(int(os.environ.get("MAX_JOBS", "8")), 16))
     for src in sources():          # one hipcc per translation unit, at most `jobs` at once
