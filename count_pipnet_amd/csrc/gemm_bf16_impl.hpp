@@ -347,13 +347,14 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
 // every SIMD one wave's MFMA segment coincides with its partner's read / DMA / barrier
 // segment and the matrix pipe alternates between the two instead of both stalling together.
 //
-// LDS: 4 stages x (256 A rows + 256 B rows) x 64 B.  K-tile t+3 is fetched (4 x 1 KiB
-// pieces per wave) at the top of phase 1 of K-tile t into the stage of K-tile t-1: every
-// wave retired its reads of t-1 (compiler lgkmcnt before the MFMAs of the phase that read
-// them) before the barrier the DMA issue follows, for both groups (derivation in DESIGN.md).
-// Each wave waits for its own pieces of K-tile t+1 (vmcnt counting the 4 or 8 younger
-// pieces) before the first barrier of phase 1 of K-tile t; group 0 reads t+1 after its next
-// barrier, group 1 one barrier later -- both after every wave's wait.
+// LDS: 4 stages x (256 A rows + 256 B rows) x 64 B.  Each phase issues 2 x 1 KiB LDS-DMA
+// pieces per wave: B of K-tile t+2 in phase 0 of K-tile t (into the stage of t-2, read by
+// everyone long before), A of K-tile t+3 in phase 1 (into the stage of t-1: every wave
+// retired its reads of t-1 -- compiler lgkmcnt before the MFMAs of the phase that read
+// them -- before the barrier this DMA issue follows, for both groups).  Each wave waits for
+// its own pieces of K-tile t+1 (vmcnt counting the 6 / 4 / 0 younger pieces) before the
+// first barrier of phase 1 of K-tile t; group 0 reads t+1 after its next barrier, group 1
+// one barrier later -- both after every wave's wait.
 //
 // Rows are 64 B (4 x 16-B chunks); chunk c of row r lives at physical chunk c ^ g(r),
 // g(r) = (-(r >> 2)) & 3: with the 16x16x32 operand map (lane l reads row l & 15, chunk
@@ -425,22 +426,24 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
       }
     }
   };
-  auto stage = [&](int kt) {                                   // 4 x 1 KiB pieces of this wave, in order
+  auto stage_a = [&](int kt) {                                 // 2 x 1 KiB A pieces of this wave
     unsigned char* base = smem + (kt & (NS - 1)) * STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a_src(ar[i], kt * BK),
                                        (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
                                        0, 0);
+    advance();
+  };
+  auto stage_b = [&](int kt) {                                 // 2 x 1 KiB B pieces of this wave
+    unsigned char* base = smem + (kt & (NS - 1)) * STAGE_BYTES;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
                                        (__attribute__((address_space(3))) void*)(base + BM * ROWB +
                                                                                  (wid + 8 * i) * 1024),
                                        16, 0, 0);
-    advance();
   };
-
   // ---- fragment reads: lane reads row (l & 15) of a 16-row block, logical chunk l >> 4 ----
   const int fr = lane & 15;
   const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));     // byte offset inside a 16-row block
@@ -461,9 +464,12 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: K-tiles 0..2 in flight, wait for tile 0 (8 younger pieces at most)
-  for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0);
-  if (nk >= 3) pp_wait_vm<8>();
+  // prologue: A(0) B(0) A(1) B(1) A(2) in flight (B(kt+2) is fetched in phase 0 of K-tile
+  // kt, A(kt+3) in phase 1: two pieces per phase), wait for tile 0
+  stage_a(0), stage_b(0);
+  if (nk > 1) stage_a(1), stage_b(1);
+  if (nk > 2) stage_a(2);
+  if (nk > 2) pp_wait_vm<6>();
   else if (nk == 2) pp_wait_vm<4>();
   else pp_wait_vm<0>();
   pp_barrier();
@@ -473,6 +479,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   for (int kt = 0; kt < nk; ++kt) {
     const unsigned char* st = smem + (kt & (NS - 1)) * STAGE_BYTES;
     // ---- phase 0: rows 0..63 of the wave's block ----
+    if (kt + 2 < nk) stage_b(kt + 2);                          // DMA before the reads (M0 write)
     read_b(fb, st);
     read_a(fa, st, 0);
     pp_barrier();
@@ -483,13 +490,13 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
       for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     pp_barrier();
-    // ---- phase 1: rows 64..127; fetch K-tile kt+3 (DMA first: an M0 write for the DMA
+    // ---- phase 1: rows 64..127; fetch A of K-tile kt+3 (DMA first: an M0 write for the DMA
     // would otherwise wait for this phase's fragment reads); wait for K-tile kt+1 ----
-    if (kt + 3 < nk) stage(kt + 3);
+    if (kt + 3 < nk) stage_a(kt + 3);
     read_a(fa, st, 1);
-    const int younger = (kt + 3 < nk ? kt + 3 : nk - 1) - (kt + 1);   // tiles issued after kt+1
-    if (younger >= 2) pp_wait_vm<8>();
-    else if (younger == 1) pp_wait_vm<4>();
+    // pieces issued after B(kt+1) (the last of K-tile kt+1): A(kt+2), B(kt+2), A(kt+3)
+    if (kt + 3 < nk) pp_wait_vm<6>();
+    else if (kt + 2 < nk) pp_wait_vm<4>();
     else pp_wait_vm<0>();
     pp_barrier();
     __builtin_amdgcn_s_setprio(1);
