@@ -20,6 +20,7 @@ using CfgM = Cfg<2, 2, 2, 2>;          // 128 x 128, 256 threads, 64 KiB LDS, 2 
 using CfgL = Cfg<2, 4, 4, 2>;          // 256 x 256, 512 threads, 128 KiB LDS, 1 workgroup / CU
 using CfgL4 = Cfg<2, 4, 4, 2, 32, 4>;  // 256 x 256, BK 32 x 4 stages (3 tiles in flight), 128 KiB
 using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2 workgroups / CU
+using CfgN64 = Cfg<4, 1, 2, 2, 32, 4>; // 256 x 64 (N = 64 layers), BK 32 x 4 stages, 80 KiB, 2 workgroups / CU
 
 // Tile choice: the largest tile that still gives every CU at least one workgroup (larger
 // tiles halve the L2 -> LDS bytes per MFMA: 128x128 needs ~64 B/clk/CU at the MFMA rate,
@@ -32,6 +33,7 @@ using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2
 // choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
 int conv_variant(int M, int N, bool pp_ok) {
   if (N >= 256 && pp_ok) return 5;
+  if (N <= 64) return 6;          // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (N >= 256 && tl >= 256) return 3;
@@ -43,7 +45,7 @@ template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
   if (v < 0) v = conv_variant(p.M, p.N, pp_ok);
-  if (v > 5 || (v == 5 && !pp_ok)) return PIPNET_ERR_ARG;
+  if (v > 6 || (v == 5 && !pp_ok)) return PIPNET_ERR_ARG;
   if (v == 5) {
     p.nt = (p.N + 255) / 256;
     p.mt = (p.M + 255) / 256;
@@ -63,7 +65,8 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }
-  const int bm = (v == 2 || v == 3) ? 256 : (v == 0 ? 64 : 128), bn = (v == 2 || v == 3) ? 256 : 128;
+  const int bm = (v == 2 || v == 3 || v == 6) ? 256 : (v == 0 ? 64 : 128),
+            bn = (v == 2 || v == 3) ? 256 : (v == 6 ? 64 : 128);
   p.nt = (p.N + bn - 1) / bn;
   p.mt = (p.M + bm - 1) / bm;
   p.group_m = choose_group_m(p.K);
@@ -73,6 +76,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     if (v == 2) hipLaunchKernelGGL((conv_bf16_kernel<CfgL, E, ALOAD, 1>), grid, dim3(512), 0, s, p);  \
     else if (v == 3) hipLaunchKernelGGL((conv_bf16_kernel<CfgL4, E, ALOAD, 1>), grid, dim3(512), 0, s, p); \
     else if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
+    else if (v == 6) hipLaunchKernelGGL((conv_bf16_kernel<CfgN64, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else if (v == 1) hipLaunchKernelGGL((conv_bf16_kernel<CfgM, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p);        \
     break;

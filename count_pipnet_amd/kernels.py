@@ -170,9 +170,12 @@ def _chk_bf(t: Tensor, what: str) -> None:
 def bf16_conv_tile(m: int, n: int, pp_ok: bool = True) -> int:
     """Workgroup tile the library picks (mirrors conv_variant in csrc/conv_bf16.hip):
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every N >= 256 layer with Cin % 32 == 0, any M),
-    else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all 32-deep K tiles in 4 LDS stages."""
+    6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
+    MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
     if n >= 256 and pp_ok:
         return 5
+    if n <= 64:
+        return 6
     if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
         return 3
     return 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
@@ -180,7 +183,7 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True) -> int:
 
 _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
              2: ("pipnet_bf16::Cfg<2, 4, 4, 2, 64, 2>", 1), 3: ("pipnet_bf16::Cfg<2, 4, 4, 2, 32, 4>", 1),
-             4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2)}
+             4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2), 6: ("pipnet_bf16::Cfg<4, 1, 2, 2, 32, 4>", 2)}
 
 
 def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True) -> str:

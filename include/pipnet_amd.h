@@ -102,8 +102,9 @@ int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const v
 /* Same, with the workgroup tile forced (tuning / tests): tile 0 = 64x128 (32-deep K tiles,
  * 4 LDS stages), 1 = 128x128 and 2 = 256x256 (64-deep, 2 stages), 3 = 256x256 and
  * 4 = 128x128 (32-deep, 4 stages), 5 = 256x256 ping-pong on 16x16x32 MFMAs (Cin % 32 == 0
- * unless 1x1 stride 1), -1 = automatic (what pipnet_conv2d_nhwc_bf16 uses: tile 5 for every
- * N >= 256 layer it can serve, whatever M; the choice never depends on the batch size, so
+ * unless 1x1 stride 1), 6 = 256x64 (32-deep, 4 stages), -1 = automatic (what
+ * pipnet_conv2d_nhwc_bf16 uses: tile 5 for every N >= 256 layer it can serve, tile 6 for
+ * N <= 64, whatever M; the MFMA shape and K order never depend on the batch size, so
  * neither do the results). */
 int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
                                  const float* bias, int Cout, int KH, int KW, int stride, int pad,

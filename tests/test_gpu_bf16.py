@@ -68,15 +68,19 @@ def test_conv2d_nhwc_bf16(gpu, cin, cout, h, k, s, pad, epi):
     _close_bf16(out.cpu(), ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
     (64, 256, 19, 3, 1, 1, _lib.EPI_BIAS_RESID_RELU),   # M = 1083: ragged in every tile size
     (256, 520, 10, 1, 2, 0, _lib.EPI_BIAS),             # N = 520: ragged N tile, strided 1x1
     (96, 264, 21, 1, 1, 0, _lib.EPI_BIAS_RELU),         # dense 1x1, K = 96 -> 128 padded (K tail of zeros)
     (512, 512, 12, 3, 1, 1, _lib.EPI_BIAS_RELU),        # layer4 3x3: 144 K-tiles, padding taps
+    (8, 64, 37, 7, 2, 3, _lib.EPI_BIAS_RELU),           # stem 7x7 s2, K 392 -> 448 (taps straddle K tiles)
+    (64, 40, 17, 3, 1, 1, _lib.EPI_BIAS),               # N = 40 < 64: ragged N in the 256x64 tile
 ])
 def test_conv2d_nhwc_bf16_every_tile(gpu, tile, cin, cout, h, k, s, pad, epi):
-    """Each workgroup tile (64x128, 128x128, 256x256, ping-pong 256x256) forced on ragged shapes."""
+    """Each workgroup tile (64x128, 128x128, 256x256, ping-pong 256x256, 256x64) forced on ragged shapes."""
+    if tile == 5 and not ((k == 1 and s == 1 and pad == 0) or cin % 32 == 0):
+        pytest.skip("the ping-pong tile needs whole-tap K tiles (Cin % 32 == 0)")
     g = torch.Generator().manual_seed(tile * 11 + cout)
     x = _bf(torch.randn(3, cin, h, h, generator=g))
     w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
