@@ -4,6 +4,8 @@
 //   * layernorm LayerNorm2d in front of each downsample conv
 // torchvision semantics restated in SURVEY.md 2.3; the reference builds the net in
 // features/convnext_features.py:38-94.
+#include <algorithm>
+
 #include "common.hpp"
 #include "convnext_dw.hpp"
 
@@ -12,71 +14,120 @@ namespace {
 constexpr float LN_EPS = 1e-6f;
 
 // ---------------------------------------------------------------------------------------
-// stem: one workgroup per (image, output row).  Input rows and transposed weights in LDS;
-// thread = (4-channel quad, pixel group), float4 accumulators; the raw row goes back through
-// LDS for the LayerNorm (one wave per pixel) so the NHWC row is written fully coalesced.
+// stem: the 4x4/s4 conv is a [96 x 48] x [48 x pixels] product -> fp32 MFMA 32x32x2 with the
+// weights as the A operand, held in 72 VGPRs per lane for the wave's lifetime, and 32 pixels
+// per tile as B.  D[channel][pixel] leaves each lane with 48 channels of ONE pixel (lanes l and
+// l+32 share it), so LayerNorm2d is a per-lane sum plus one xor-32 shuffle.  (Replaced two
+// VALU kernels -- weights broadcast from LDS, then from SGPRs -- whose operand latency left
+// the C2 stem at 93-115 us; this one is MFMA/HBM-bound.)
 // ---------------------------------------------------------------------------------------
-constexpr int STEM_C = 96, STEM_K = 48, STEM_Q = STEM_C / 4, STEM_G = 10, STEM_NPX = 6;
-constexpr int STEM_OLD = STEM_C + 4;       // padded LDS row of the raw output tile
+constexpr int STEM_C = 96, STEM_K = 48, STEM_T = 256, STEM_TILE = 32;
 
-__global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W,
-                                                   const float* __restrict__ w, const float* __restrict__ bias,
-                                                   const float* __restrict__ lnw, const float* __restrict__ lnb,
-                                                   float* __restrict__ y) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
+// K order: MFMA step s = (ci*2 + u)*4 + kx sums kernel row ky = u (lanes 0-31) and ky = 2 + u
+// (lanes 32-63), so each lane fetches whole 4-pixel input rows (6 float4 per tile) and its
+// weights as 8 contiguous floats per (block, ci) (18 float4 per wave lifetime).
+__global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(2, 2))) void stem_kernel(const float* __restrict__ x, int B, int H, int W,
+                                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                                      const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                      float* __restrict__ y, int64_t ntiles) {
+  const int lane = threadIdx.x & 63, h = lane >> 5, n = lane & 31;
   const int OH = H / 4, OW = W / 4;
-  float* wsm = sm;                                 // [48][96]  (k-major: float4 over channels)
-  float* otile = wsm + STEM_K * STEM_C;            // [OW][100]
-  float* xin = otile + OW * STEM_OLD;              // [3][4][W]
-  const int b = blockIdx.x / OH, oy = blockIdx.x - (blockIdx.x / OH) * OH;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < STEM_C * STEM_K; i += 256) {
-    const int c = i / STEM_K, k = i - c * STEM_K;
-    wsm[k * STEM_C + c] = w[i];
-  }
-  const int w4 = W / 4;
-  for (int i = tid; i < 12 * w4; i += 256) {
-    const int r = i / w4, xx = i - r * w4;          // r = c*4 + ky
-    const int c = r >> 2, ky = r & 3;
-    st4(xin + r * W + 4 * xx, ld4(x + (((int64_t)b * 3 + c) * H + 4 * oy + ky) * W + 4 * xx));
-  }
+  const int64_t npx = (int64_t)B * OH * OW;
+  float wa[3][24];                                   // A operand: w[32*blk + n][ci*16 + (2h+u)*4 + kx]
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const f32x4 v = ld4(w + (32 * blk + n) * STEM_K + ci * 16 + (2 * h + u) * 4);
+#pragma unroll
+        for (int kx = 0; kx < 4; ++kx) wa[blk][(ci * 2 + u) * 4 + kx] = v[kx];
+      }
+  // bias / LayerNorm affine in LDS: their per-tile reads must not sit in the vmcnt queue behind
+  // the next tile's prefetch (vmcnt retires in order), nor be hoisted into 144 VGPRs
+  __shared__ __attribute__((aligned(16))) float vec_sm[3 * STEM_C];
+  for (int i = threadIdx.x; i < 3 * STEM_C; i += STEM_T)
+    vec_sm[i] = i < STEM_C ? bias[i] : i < 2 * STEM_C ? lnw[i - STEM_C] : lnb[i - 2 * STEM_C];
   __syncthreads();
-  const int q = tid % STEM_Q, g = tid / STEM_Q;
-  if (g < STEM_G) {
-    const f32x4 bq = ld4(bias + 4 * q);
-    for (int px0 = g; px0 < OW; px0 += STEM_G * STEM_NPX) {
-      f32x4 acc[STEM_NPX];
+  const int64_t nwaves = (int64_t)gridDim.x * (STEM_T / 64);
+  // B operand: x[pixel n][ci][2h + u][kx] as xv[ci*2 + u][kx].  Lanes past the last pixel load
+  // the last pixel instead (branch-free, so the prefetch stays where it is issued); a D column
+  // only ever feeds its own pixel's LayerNorm and store, so those lanes' results are dropped.
+  auto load_tile = [&](int64_t tile, f32x4 (&xv)[6]) {
+    const int64_t p = std::min<int64_t>(tile * STEM_TILE + n, npx - 1);
+    const int b = (int)(p / ((int64_t)OH * OW));
+    const int rem = (int)(p - (int64_t)b * OH * OW);
+    const int oy = rem / OW, ox = rem - oy * OW;
+    const float* src = x + (((int64_t)b * 3) * H + 4 * oy + 2 * h) * W + 4 * ox;
 #pragma unroll
-      for (int p = 0; p < STEM_NPX; ++p) acc[p] = bq;
-#pragma unroll 4
-      for (int k = 0; k < STEM_K; ++k) {
-        const f32x4 wk = ld4(wsm + k * STEM_C + 4 * q);
-        const float* xr = xin + (k >> 2) * W + (k & 3);   // (c*4+ky) row, kx column offset
+    for (int ci = 0; ci < 3; ++ci)
 #pragma unroll
-        for (int p = 0; p < STEM_NPX; ++p) {
-          const int px = px0 + p * STEM_G;
-          const float v = px < OW ? xr[4 * px] : 0.f;
-          acc[p] += v * wk;
+      for (int u = 0; u < 2; ++u) xv[ci * 2 + u] = ld4(src + ((int64_t)ci * H + u) * W);
+  };
+  int64_t tile = (int64_t)blockIdx.x * (STEM_T / 64) + (threadIdx.x >> 6);
+  f32x4 xv[6];
+  load_tile(tile, xv);
+  for (; tile < ntiles; tile += nwaves) {
+    const int64_t p = tile * STEM_TILE + n;
+    const bool ok = p < npx;
+    int z = 0;                                       // opaque 0: keeps the LDS reads per tile
+    asm volatile("" : "+v"(z));
+    const float* bias_t = vec_sm + z;
+    const float* lnw_t = vec_sm + STEM_C + z;
+    const float* lnb_t = vec_sm + 2 * STEM_C + z;
+    float xb[24];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) xb[q * 4 + kx] = xv[q][kx];
+    load_tile(tile + nwaves, xv);                    // next tile's loads fly under this one's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
+    f32x16 acc[3];
+#pragma unroll
+    for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {                  // D row (channel) 32*blk + 8j + 4h + i
+        const f32x4 bv = ld4(bias_t + 32 * blk + 8 * j + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[blk][4 * j + i] = bv[i];
+      }
+#pragma unroll
+    for (int k = 0; k < 24; ++k)
+#pragma unroll
+      for (int blk = 0; blk < 3; ++blk)
+        acc[blk] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[blk][k], xb[k], acc[blk], 0, 0, 0);
+    float s = 0.f;
+#pragma unroll
+    for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s += acc[blk][i];
+    s += __shfl_xor(s, 32, 64);
+    const float mean = s * (1.0f / STEM_C);
+    float qq = 0.f;
+#pragma unroll
+    for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float d = acc[blk][i] - mean;
+        qq = fmaf(d, d, qq);
+      }
+    qq += __shfl_xor(qq, 32, 64);
+    const float rstd = 1.0f / sqrtf(qq * (1.0f / STEM_C) + LN_EPS);
+    if (ok) {
+      float* dst = y + p * STEM_C;
+#pragma unroll
+      for (int blk = 0; blk < 3; ++blk)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = 32 * blk + 8 * j + 4 * h;
+          const f32x4 gw = ld4(lnw_t + c), gb = ld4(lnb_t + c);
+          f32x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = (acc[blk][4 * j + i] - mean) * rstd * gw[i] + gb[i];
+          st4(dst + c, o);
         }
-      }
-#pragma unroll
-      for (int p = 0; p < STEM_NPX; ++p) {
-        const int px = px0 + p * STEM_G;
-        if (px < OW) st4(otile + px * STEM_OLD + 4 * q, acc[p]);
-      }
     }
-  }
-  __syncthreads();
-  const int lane = tid & 63, wv = tid >> 6;
-  for (int px = wv; px < OW; px += 4) {
-    const float v0 = otile[px * STEM_OLD + lane];
-    const float v1 = lane < 32 ? otile[px * STEM_OLD + 64 + lane] : 0.f;
-    const float mean = wave_sum(v0 + v1) * (1.0f / STEM_C);
-    const float d0 = v0 - mean, d1 = lane < 32 ? v1 - mean : 0.f;
-    const float rstd = 1.0f / sqrtf(wave_sum(d0 * d0 + d1 * d1) * (1.0f / STEM_C) + LN_EPS);
-    float* dst = y + (((int64_t)b * OH + oy) * OW + px) * STEM_C;
-    dst[lane] = d0 * rstd * lnw[lane] + lnb[lane];
-    if (lane < 32) dst[64 + lane] = d1 * rstd * lnw[64 + lane] + lnb[64 + lane];
   }
 }
 
@@ -120,13 +171,17 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 
 extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, const float* w, const float* b,
                                         const float* ln_w, const float* ln_b, float* y, void* stream) {
-  if (B < 0 || H < 4 || W < 4 || (H & 3) || (W & 3) || W > 960) return PIPNET_ERR_ARG;
+  if (B < 0 || H < 4 || W < 4 || (H & 3) || (W & 3)) return PIPNET_ERR_ARG;
   if (!x || !w || !b || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
-  if (!aligned16(x) || !aligned16(y) || !aligned16(b)) return PIPNET_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(w) || !aligned16(y) || !aligned16(b) || !aligned16(ln_w) || !aligned16(ln_b))
+    return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
-  const size_t shmem = (STEM_K * STEM_C + (W / 4) * STEM_OLD + 12 * W) * sizeof(float);
-  hipLaunchKernelGGL(stem_kernel, dim3(B * (H / 4)), dim3(256), shmem, (hipStream_t)stream, x, H, W, w, b, ln_w,
-                     ln_b, y);
+  const int64_t npx = (int64_t)B * (H / 4) * (W / 4);
+  const int64_t ntiles = (npx + STEM_TILE - 1) / STEM_TILE;
+  // at most 2 waves per SIMD (its occupancy), each looping over tiles with the weights in registers
+  const int64_t grid = std::min<int64_t>((ntiles + STEM_T / 64 - 1) / (STEM_T / 64), 256 * 2);
+  hipLaunchKernelGGL(stem_kernel, dim3((unsigned)grid), dim3(STEM_T), 0, (hipStream_t)stream,
+                     x, B, H, W, w, b, ln_w, ln_b, y, ntiles);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

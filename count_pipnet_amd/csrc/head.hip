@@ -227,7 +227,8 @@ PIPNET_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
   return (uint32_t)p;
 }
 
-PIPNET_DEV float philox_exp(uint64_t seed, uint64_t ctr) {
+// One Philox4x32-10 block: four 32-bit words for counter `ctr` under key `seed`.
+PIPNET_DEV void philox4(uint64_t seed, uint64_t ctr, uint32_t (&out)[4]) {
   uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0u, c3 = 0u;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
 #pragma unroll
@@ -242,10 +243,20 @@ PIPNET_DEV float philox_exp(uint64_t seed, uint64_t ctr) {
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-  const float u = ((float)(c0 >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  out[0] = c0, out[1] = c1, out[2] = c2, out[3] = c3;
+}
+
+PIPNET_DEV float exp1_from_bits(uint32_t w) {
+  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
   return -logf(u);
 }
 
+// One wave per pixel, four consecutive channels per lane (float4 logits / proto): the noise
+// of channels 4k..4k+3 of pixel (b, pix) is the Philox block (offset + (b*HW + pix)*P/4 + k)
+// -- one block per four elements, no word wasted.  Per pixel: z = (x - log E) / tau, argmax
+// (first index on ties), y_soft at the argmax = 1 / sum exp(z - max), one-hot written as
+// (1 - y_soft) + y_soft (F.gumbel_softmax(hard=True)'s straight-through value).
+// P % 4 == 0.
 template <int NJ>
 __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float* __restrict__ logits, int HW, int P,
                                                                     float inv_tau,
@@ -254,7 +265,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
                                                                     const uint64_t* __restrict__ seed_dev,
                                                                     float* __restrict__ proto,
                                                                     int32_t* __restrict__ hist) {
-  if (seed_dev) seed = *seed_dev;     // graph-replay form: the seed lives in device memory
+  constexpr int NJ4 = (NJ + 3) / 4;         // float4 channel chunks per lane (256 channels each)
+  if (seed_dev) seed = *seed_dev;            // graph-replay form: the seed lives in device memory
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int pix0 = blockIdx.x * PIX_PER_BLOCK;
@@ -262,19 +274,32 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
     const int pix = pix0 + pi;
     if (pix >= HW) break;
     const int64_t base = ((int64_t)b * HW + pix) * P;
-    float z[NJ];
+    float z[NJ4][4];
     float m = -INFINITY;
     int mi = 0x7fffffff;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
+    for (int j = 0; j < NJ4; ++j) {
+      const int c = 4 * lane + 256 * j;
       if (c < P) {
-        const int64_t e_idx = ((int64_t)b * P + c) * HW + pix;      // NCHW element index
-        const float E = exp_noise ? exp_noise[e_idx] : philox_exp(seed, offset + (uint64_t)e_idx);
-        z[j] = (logits[base + c] - logf(E)) * inv_tau;
-        if (z[j] > m) { m = z[j]; mi = c; }
+        const f32x4 x = ld4(logits + base + c);
+        float E[4];
+        if (exp_noise) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) E[e] = exp_noise[((int64_t)b * P + c + e) * HW + pix];   // NCHW draw
+        } else {
+          uint32_t w[4];
+          philox4(seed, offset + (uint64_t)((base + c) >> 2), w);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) E[e] = exp1_from_bits(w[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          z[j][e] = (x[e] - logf(E[e])) * inv_tau;
+          if (z[j][e] > m) { m = z[j][e]; mi = c + e; }
+        }
       } else {
-        z[j] = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) z[j][e] = -INFINITY;
       }
     }
     // wave argmax, first index on ties
@@ -284,15 +309,22 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
       const int oi = __shfl_xor(mi, o, 64);
       if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
     }
-    float s = 0.f;
+    float sum = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) s += (lane + 64 * j < P) ? expf(z[j] - m) : 0.f;
-    const float ysoft = 1.0f / wave_sum(s);              // softmax value at the argmax
-    const float hard = (1.0f - ysoft) + ysoft;           // y_hard - y_soft + y_soft
+    for (int j = 0; j < NJ4; ++j)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      if (c < P) proto[base + c] = (c == mi) ? hard : 0.f;
+      for (int e = 0; e < 4; ++e) sum += (4 * lane + 256 * j < P) ? expf(z[j][e] - m) : 0.f;
+    const float ysoft = 1.0f / wave_sum(sum);              // softmax value at the argmax
+    const float hard = (1.0f - ysoft) + ysoft;             // y_hard - y_soft + y_soft
+#pragma unroll
+    for (int j = 0; j < NJ4; ++j) {
+      const int c = 4 * lane + 256 * j;
+      if (c < P) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (c + e == mi) ? hard : 0.f;
+        st4(proto + base + c, o);
+      }
     }
     if (lane == 0) atomicAdd(hist + (int64_t)b * P + mi, 1);
   }
@@ -422,7 +454,8 @@ extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const floa
 namespace {
 int count_gumbel_launch(const float* logits, int B, int HW, int P, float tau, const float* exp_noise, uint64_t seed,
                         uint64_t offset, const uint64_t* seed_dev, float* proto, int32_t* hist, void* stream) {
-  if (B < 0 || HW <= 0 || P <= 0 || !(tau > 0.f) || !logits || !proto || !hist) return PIPNET_ERR_ARG;
+  if (B < 0 || HW <= 0 || P <= 0 || (P & 3) || !(tau > 0.f) || !logits || !proto || !hist) return PIPNET_ERR_ARG;
+  if (!aligned16(logits) || !aligned16(proto)) return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
   const int nj = nj_bucket(P);
   if (nj < 0) return PIPNET_ERR_ARG;

@@ -141,7 +141,7 @@ int pipnet_weight_sparsify_f32(float* w, int64_t n, float delta, void* stream);
 
 /* ConvNeXt stem: Conv2d(3,96,k4,s4,bias) + LayerNorm2d(96, eps 1e-6)  (features.0).
  * x: [B,3,H,W] NCHW (the reference's own input layout), w: [96,3,4,4] as torch stores it,
- * y: [B,H/4,W/4,96] NHWC. */
+ * y: [B,H/4,W/4,96] NHWC.  H, W multiples of 4; x, w, b, ln_w, ln_b, y 16-byte aligned. */
 int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, const float* w, const float* b,
                              const float* ln_w, const float* ln_b, float* y, void* stream);
 
@@ -176,8 +176,9 @@ int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const
  * count_pipnet.py:88): per pixel z = (x - log E)/tau, one-hot at argmax written as the
  * straight-through value (1 - y) + y, all other channels exactly 0, and hist[b,p] += 1.
  * E ~ Exp(1) is read from exp_noise ([B,P,HW], the NCHW layout of torch's draw) when
- * non-NULL, else generated in-kernel by Philox4x32-10 keyed by (seed, offset + element).
- * logits, proto: [B,HW,P]; hist: [B,P] int32 (zeroed by this call). */
+ * non-NULL, else generated in-kernel by Philox4x32-10 keyed by (seed, offset + element/4):
+ * one 128-bit block feeds channels 4k..4k+3 of a pixel.
+ * logits, proto: [B,HW,P], 16-byte aligned, P % 4 == 0; hist: [B,P] int32 (zeroed by this call). */
 int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau,
                             const float* exp_noise, uint64_t seed, uint64_t offset, float* proto,
                             int32_t* hist, void* stream);

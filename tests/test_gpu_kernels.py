@@ -83,10 +83,12 @@ def test_conv2x2(gpu, cin, cout, h, stride):
     assert torch.allclose(out, ref, rtol=2e-5, atol=2e-5), (out - ref).abs().max()
 
 
-@pytest.mark.parametrize("h", [224, 64, 128])
-def test_stem(gpu, h):
-    g = torch.Generator().manual_seed(h)
-    x, w, b = _rand(2, 3, h, h, gen=g), _rand(96, 3, 4, 4, gen=g, scale=0.2), _rand(96, gen=g)
+@pytest.mark.parametrize("bsz,h,wd", [(2, 224, 224), (2, 64, 64), (2, 128, 128), (3, 36, 20), (1, 4, 8), (5, 68, 132)])
+def test_stem(gpu, bsz, h, wd):
+    """MFMA stem: 32-pixel tiles, so pixel counts that are not a multiple of 32 (3*9*5, 1*1*2,
+    5*17*33) exercise the ragged last tile; non-square images the (oy, ox) decomposition."""
+    g = torch.Generator().manual_seed(h * 1000 + wd)
+    x, w, b = _rand(bsz, 3, h, wd, gen=g), _rand(96, 3, 4, 4, gen=g, scale=0.2), _rand(96, gen=g)
     lw, lb = 1 + 0.1 * _rand(96, gen=g), 0.1 * _rand(96, gen=g)
     y = F.conv2d(x, w, b, stride=4).permute(0, 2, 3, 1)
     ref = F.layer_norm(y, (96,), lw, lb, 1e-6)
