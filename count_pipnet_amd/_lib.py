@@ -18,12 +18,14 @@ I32 = ctypes.c_int
 I64 = ctypes.c_int64
 U64 = ctypes.c_uint64
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 
 # name -> argtypes (restype is int status unless listed in _RESTYPE)
 SIGNATURES = {
     "pipnet_amd_abi_version": [],
     "pipnet_amd_status_string": [I32],
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
+    "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],
     "pipnet_linear_splitk_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, I32, P, P],
     "pipnet_conv2x2_f32": [P, I32, I32, I32, I32, P, P, I32, I32, P, P],
     "pipnet_convnext_stem_f32": [P, I32, I32, I32, P, P, P, P, P, P],
@@ -47,10 +49,17 @@ SIGNATURES = {
     "pipnet_count_encode_f32": [P, I32, I32, I32, I32, I32, P, P, P],
     "pipnet_resize_plan": [P, I32, I32, I32, P, P],
     "pipnet_resize_normalize_rgb8": [P, P, P, I32, I32, I32, I32, I32, P, P, P, P, P, P],
+    "pipnet_train_align_partials": [],
+    "pipnet_train_align_partial_f32": [P, I32, I32, I32, P, P],
+    "pipnet_train_loss_f32": [P, I32, I32, P, P, P, I32, I32, P, I32, F32, F32, F32, F32, I32, P, P, P],
+    "pipnet_nonneg_linear_bwd_f32": [P, P, I32, I32, P, I32, P, P, P],
+    "pipnet_adamw_step_f32": [P, P, P, P, I64, F64, F64, F64, F64, F64, I64, I32, F32, F32, P],
+    "pipnet_clamp_min_f32": [P, I64, F32, P],
 }
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p}
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
+EPI_RESID_ROWSCALE = 7
 
 _lib = None
 

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import os
 import warnings
-from typing import Dict
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.nn as nn
@@ -232,7 +232,12 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
     return ent[1]
 
 
-def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str) -> Tensor:
+def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Optional[Tensor] = None) -> Tensor:
+    """One CNBlock in place on NHWC ``h``.  ``row_scale`` (train mode, StochasticDepth "row"):
+    device [B] = keep_b / (1 - p); the Linear2 epilogue scales each sample's branch by it
+    (0 leaves a dropped sample's rows equal to the residual), so the batch stays one
+    full-size GEMM (splitting it into kept runs measured slower: small-M grids underfill
+    the 256 CUs)."""
     dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
     b, hh, ww, c = h.shape
     if dw.kernel_size != (7, 7) or dw.padding != (3, 3) or dw.groups != c or dw.stride != (1, 1):
@@ -241,15 +246,42 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str) -> Tensor:
     t = K.dwconv7_ln(h, wdw, dw.bias, ln.weight, ln.bias)
     u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS_GELU)
     hv = h.view(-1, c)
-    K.linear(u, l2.weight, l2.bias, _lib.EPI_RESID, scale=blk.layer_scale.view(-1), r=hv, out=hv)
+    if row_scale is None:
+        K.linear(u, l2.weight, l2.bias, _lib.EPI_RESID, scale=blk.layer_scale.view(-1), r=hv, out=hv)
+    else:
+        K.linear_rowscale(u, l2.weight, l2.bias, blk.layer_scale.view(-1), hv, row_scale, hh * ww)
     return h
 
 
-def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict) -> Tensor:
-    """Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels."""
+def stochastic_depth_row_scales(features: nn.Sequential, sd_keep: Dict[int, object], batch: int,
+                                device) -> Dict[int, Tensor]:
+    """Per-block device vectors keep_b / (1 - p) (float32, as StochasticDepth's
+    ``noise.div_(1 - p)``) for the blocks with p > 0, staged through one pinned buffer and
+    one asynchronous copy (no per-block synchronisation)."""
+    blocks = [blk for mod in features if isinstance(mod, nn.Sequential) for blk in mod if isinstance(blk, CNBlock)]
+    ids = [bid for bid, blk in enumerate(blocks) if blk.stochastic_depth.p > 0.0]
+    if not ids:
+        return {}
+    host = torch.empty((len(ids), batch), dtype=torch.float32, pin_memory=torch.device(device).type == "cuda")
+    for j, bid in enumerate(ids):
+        mask = torch.as_tensor(sd_keep[bid]).reshape(-1)
+        if mask.numel() != batch:
+            raise RuntimeError(f"stochastic-depth mask of block {bid} has {mask.numel()} entries for batch {batch}")
+        host[j] = mask.to(torch.float32).div_(1.0 - blocks[bid].stochastic_depth.p)
+    dev = host.to(device, non_blocking=True)
+    return {bid: dev[j] for j, bid in enumerate(ids)}
+
+
+def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
+                          sd_keep: Optional[Dict[int, object]] = None) -> Tensor:
+    """Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels.
+    ``sd_keep``: train-mode stochastic depth, block id (0..17 in module order) -> per-sample
+    keep mask for every block with p > 0 (eval / None: no stochastic depth)."""
     K.require_device(x, "network input")
     x = x.contiguous()
     h = None
+    bid = 0
+    scales = None if sd_keep is None else stochastic_depth_row_scales(features, sd_keep, x.shape[0], x.device)
     for idx, mod in enumerate(features):
         name = str(idx)
         if idx == 0:
@@ -259,7 +291,8 @@ def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict) -> Te
             h = K.convnext_stem(x, conv.weight, conv.bias, ln.weight, ln.bias)
         elif len(mod) > 0 and isinstance(mod[0], CNBlock):
             for j, blk in enumerate(mod):
-                h = _cnblock_hip(blk, h, cache, f"{name}.{j}")
+                h = _cnblock_hip(blk, h, cache, f"{name}.{j}", None if scales is None else scales.get(bid))
+                bid += 1
         elif len(mod) == 2 and isinstance(mod[0], LayerNorm2d) and isinstance(mod[1], nn.Conv2d):
             ln, conv = mod[0], mod[1]
             if conv.kernel_size != (2, 2) or conv.padding != (0, 0):

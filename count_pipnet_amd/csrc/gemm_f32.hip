@@ -74,6 +74,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
     PIPNET_EPI_CASE(PIPNET_EPI_MUL)
     PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RELU)
     PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RESID_RELU)
+    PIPNET_EPI_CASE(PIPNET_EPI_RESID_ROWSCALE)
     default: return PIPNET_ERR_ARG;
   }
 #undef PIPNET_EPI_CASE
@@ -99,6 +100,22 @@ extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, co
   p.A = A; p.lda = lda; p.W = W; p.bias = bias; p.scale = scale; p.R = R; p.ldr = ldr;
   p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
   return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_linear_rowscale_f32(const float* A, int64_t lda, const float* W, const float* bias,
+                                          const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
+                                          int M, int N, int K, const float* row_scale, int rows_per_scale,
+                                          void* stream) {
+  if (M < 0 || N < 0 || K <= 0 || rows_per_scale <= 0) return PIPNET_ERR_ARG;
+  if (M == 0 || N == 0) return PIPNET_OK;
+  if ((K & 3) || (lda & 3) || lda < K || ldc < N || !R || ldr < N) return PIPNET_ERR_ARG;
+  if (!A || !W || !C || !row_scale) return PIPNET_ERR_ARG;
+  if (!aligned16(A) || !aligned16(W)) return PIPNET_ERR_ALIGN;
+  GemmParams p{};
+  p.A = A; p.lda = lda; p.W = W; p.bias = bias; p.scale = scale; p.R = R; p.ldr = ldr;
+  p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
+  p.row_scale = row_scale; p.rows_per_scale = rows_per_scale;
+  return launch_gemm<ALOAD_DENSE>(p, PIPNET_EPI_RESID_ROWSCALE, (hipStream_t)stream);
 }
 
 extern "C" int pipnet_conv2x2_f32(const float* x, int B, int H, int W, int Cin, const float* w_packed,

@@ -50,6 +50,8 @@ struct GemmParams {
   int stagger_lo, stagger_hi;
   int64_t split_stride;   // split-K (gridDim.y > 1): slab y of C starts at C + y * split_stride
   long long* stamps;      // lab (ABL & 8): per-workgroup s_memtime stamps + hardware ids
+  const float* row_scale; // PIPNET_EPI_RESID_ROWSCALE: per row-group factor (stochastic depth)
+  int rows_per_scale;
 };
 
 // Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 8
@@ -200,7 +202,7 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
     if (n >= p.N) continue;
     float bn = 0.f, sn = 1.f;
     if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL) bn = p.bias ? p.bias[n] : 0.f;
-    if (EPI == PIPNET_EPI_RESID) sn = p.scale ? p.scale[n] : 1.f;
+    if (EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) sn = p.scale ? p.scale[n] : 1.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -211,6 +213,8 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
         if (EPI == PIPNET_EPI_BIAS) x = x + bn;
         if (EPI == PIPNET_EPI_BIAS_GELU) x = gelu_fast(x + bn);
         if (EPI == PIPNET_EPI_RESID) x = p.R[(int64_t)m * p.ldr + n] + sn * (x + bn);
+        if (EPI == PIPNET_EPI_RESID_ROWSCALE)
+          x = p.R[(int64_t)m * p.ldr + n] + p.row_scale[m / p.rows_per_scale] * (sn * (x + bn));
         if (EPI == PIPNET_EPI_MUL) x = x * p.R[(int64_t)m * p.ldr + n];
         if (EPI == PIPNET_EPI_BIAS_RELU) x = fmaxf(x + bn, 0.f);
         if (EPI == PIPNET_EPI_BIAS_RESID_RELU) x = fmaxf(x + bn + p.R[(int64_t)m * p.ldr + n], 0.f);
@@ -221,7 +225,7 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
 }
 
 template <int EPI>
-PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4& r) {
+PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4& r, float rs = 1.f) {
   if (EPI == PIPNET_EPI_BIAS) x = x + bn;
   if (EPI == PIPNET_EPI_BIAS_GELU) {      // packed A&S 7.1.28 (lab: +2..+8 % over gelu_fast)
     x = x + bn;
@@ -236,6 +240,7 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
     x = f32x4{lo[0], lo[1], hi[0], hi[1]};
   }
   if (EPI == PIPNET_EPI_RESID) x = r + sn * (x + bn);
+  if (EPI == PIPNET_EPI_RESID_ROWSCALE) x = r + rs * (sn * (x + bn));   // (ls * y) * (mask / keep) + x
   if (EPI == PIPNET_EPI_MUL) x = x * r;
   if (EPI == PIPNET_EPI_BIAS_RELU) {
     x = x + bn;
@@ -260,7 +265,8 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
 template <int EPI, int TM>
 PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, int m0, int n0, int wm, int wn,
                              int lane, int wid) {
-  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU;
+  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU ||
+                         EPI == PIPNET_EPI_RESID_ROWSCALE;
   float* wt = smem + wid * 32 * 64;
   const int lr = lane & 31, lh = lane >> 5;
   const int c4 = lane & 15;
@@ -268,7 +274,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, i
   const bool nok = n < p.N;
   f32x4 bn = {0.f, 0.f, 0.f, 0.f}, sn = {1.f, 1.f, 1.f, 1.f};
   if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && p.bias && nok) bn = ld4(p.bias + n);   // (incl. lab GELU)
-  if (EPI == PIPNET_EPI_RESID && p.scale && nok) sn = ld4(p.scale + n);
+  if ((EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) && p.scale && nok) sn = ld4(p.scale + n);
   f32x4 r[TM][8];
   if (HAS_R) {
 #pragma unroll
@@ -291,7 +297,9 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, i
     for (int it = 0; it < 8; ++it) {
       const int row = it * 4 + (lane >> 4);
       const int m = m0 + wm * 32 * TM + i * 32 + row;
-      const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn);
+      float rs = 1.f;
+      if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
+      const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
       if (m < p.M && nok) st4(p.C + (int64_t)m * p.ldc + n, x);
     }
   }

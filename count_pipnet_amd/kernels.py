@@ -105,6 +105,26 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     return out
 
 
+def linear_rowscale(a: Tensor, w: Tensor, bias: Optional[Tensor], scale: Tensor, r: Tensor, row_scale: Tensor,
+                    rows_per_scale: int) -> Tensor:
+    """In place on ``r`` ([M,N]): r = r + row_scale[m // rows_per_scale] * (scale * (a w^T + bias))
+    (CNBlock Linear2 under train-mode stochastic depth)."""
+    require_device(a, "linear input")
+    _chk(w, "weight")
+    _chk(row_scale, "row scale")
+    m, k = a.shape
+    n = w.shape[0]
+    if w.shape[1] != k or tuple(r.shape) != (m, n) or a.stride(1) != 1 or r.stride(1) != 1:
+        raise RuntimeError(f"linear_rowscale: shapes a {tuple(a.shape)}, w {tuple(w.shape)}, r {tuple(r.shape)}")
+    if row_scale.numel() * rows_per_scale < m:
+        raise RuntimeError("linear_rowscale: row_scale does not cover every row")
+    _launch(gemm_kernel_name(m, n, k, _lib.EPI_RESID_ROWSCALE, 0), 2.0 * m * n * k,
+            lambda: _lib.call("pipnet_linear_rowscale_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias),
+                              _ptr(scale), r.data_ptr(), r.stride(0), r.data_ptr(), r.stride(0), m, n, k,
+                              row_scale.data_ptr(), rows_per_scale, _stream(a)))
+    return r
+
+
 def conv2x2(x_nhwc: Tensor, w_packed: Tensor, bias: Optional[Tensor], stride: int) -> Tensor:
     _chk(x_nhwc, "conv2x2 input")
     b, h, w, cin = x_nhwc.shape
@@ -458,3 +478,75 @@ def resize_normalize_rgb8(pixels: Tensor, offsets: Tensor, sizes: Tensor, sizes_
               kmax.value, int(bool(grayscale)), m, s, ws.data_ptr(), out.data_ptr(), _ptr(out_u8),
               torch.cuda.current_stream(dev).cuda_stream)
     return (out, out_u8) if want_u8 else out
+
+
+# ---- training step, finetune phase (csrc/train_ops.hip) -------------------------------------
+TRAIN_MODE = {"train": 0, "pretrain": 1, "finetune": 2}
+
+
+def train_loss(proto_nhwc: Tensor, pooled: Tensor, out: Tensor, ys: Tensor, mult: Optional[Tensor],
+               enforce: bool, tanh_coeff: float, w_align: float, w_tanh: float, w_class: float,
+               mode: str) -> Tuple[Tensor, Optional[Tensor]]:
+    """calculate_loss (pipnet/train.py:154-250) on the device: returns (stats [8] fp32 =
+    align, tanh, class, loss, correct, w_align, w_tanh, w_class; d_out [N,K] or None)."""
+    _chk(proto_nhwc, "proto features (NHWC)")
+    _chk(pooled, "pooled")
+    _chk(out, "classifier output")
+    n, h, w, p = proto_nhwc.shape
+    if n % 2 or tuple(pooled.shape) != (n, p) or out.shape[0] != n:
+        raise RuntimeError(f"train_loss: proto {tuple(proto_nhwc.shape)}, pooled {tuple(pooled.shape)}, "
+                           f"out {tuple(out.shape)} must share an even batch = cat([xs1, xs2])")
+    bh, k = n // 2, out.shape[1]
+    if not (ys.is_cuda and ys.dtype == torch.int64 and ys.is_contiguous() and ys.shape == (bh,)):
+        raise RuntimeError("train_loss: labels must be a contiguous int64 device tensor of the half batch")
+    if mult is not None:
+        _chk(mult, "normalization_multiplier")
+    partial = torch.empty(_lib.load().pipnet_train_align_partials(), device=out.device, dtype=torch.float64)
+    s = _stream(out)
+    _lib.call("pipnet_train_align_partial_f32", proto_nhwc.data_ptr(), bh, h * w, p, partial.data_ptr(), s)
+    stats = torch.empty(8, device=out.device, dtype=torch.float32)
+    m = TRAIN_MODE[mode]
+    d_out = None if m == 1 else torch.empty_like(out)
+    _lib.call("pipnet_train_loss_f32", partial.data_ptr(), bh, h * w, pooled.data_ptr(), out.data_ptr(),
+              ys.data_ptr(), p, k, _ptr(mult), int(bool(enforce)), float(tanh_coeff), float(w_align),
+              float(w_tanh), float(w_class), m, _ptr(d_out), stats.data_ptr(), s)
+    return stats, d_out
+
+
+def nonneg_linear_backward(d_out: Tensor, x: Tensor, w: Tensor, want_bias: bool) -> Tuple[Tensor, Optional[Tensor]]:
+    """Gradients of F.linear(x, relu(w), b) (pipnet.py:54-71): (dW, db or None)."""
+    _chk(d_out, "d_out")
+    _chk(x, "classifier input")
+    _chk(w, "classifier weight")
+    n, d = x.shape
+    k = w.shape[0]
+    if tuple(w.shape) != (k, d) or tuple(d_out.shape) != (n, k):
+        raise RuntimeError("nonneg_linear_backward: shapes disagree")
+    dw = torch.empty_like(w)
+    db = torch.empty(k, device=w.device, dtype=torch.float32) if want_bias else None
+    _lib.call("pipnet_nonneg_linear_bwd_f32", d_out.data_ptr(), x.data_ptr(), n, d, w.data_ptr(), k,
+              dw.data_ptr(), _ptr(db), _stream(w))
+    return dw, db
+
+
+def adamw_step_(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor, lr: float, beta1: float,
+                beta2: float, eps: float, weight_decay: float, step: int,
+                post: Optional[Tuple[float, float]] = None) -> None:
+    """torch.optim.AdamW's update of one tensor in place at optimizer step ``step`` (1-based;
+    bias corrections from the double hyper-parameters, as torch computes them for a
+    non-capturable optimizer); ``post`` = (delta, floor) applies p = max(p - delta, floor)
+    afterwards (pipnet/train.py:134-140)."""
+    for t, what in ((param, "parameter"), (grad, "gradient"), (exp_avg, "exp_avg"), (exp_avg_sq, "exp_avg_sq")):
+        _chk(t, what)
+        if t.shape != param.shape:
+            raise RuntimeError(f"adamw_step_: {what} shape {tuple(t.shape)} != {tuple(param.shape)}")
+    delta, floor = post if post is not None else (0.0, 0.0)
+    _lib.call("pipnet_adamw_step_f32", param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
+              exp_avg_sq.data_ptr(), param.numel(), lr, beta1, beta2, eps, weight_decay, int(step),
+              int(post is not None), delta, floor, _stream(param))
+
+
+def clamp_min_(x: Tensor, lo: float) -> Tensor:
+    _chk(x, "tensor")
+    _lib.call("pipnet_clamp_min_f32", x.data_ptr(), x.numel(), lo, _stream(x))
+    return x

@@ -101,3 +101,9 @@ def synth_exponential(shape: Tuple[int, ...], seed: int) -> torch.Tensor:
     g = _rng(seed, "exp/" + "x".join(str(int(s)) for s in shape))
     a = g.standard_exponential(size=tuple(shape), dtype=np.float32)
     return torch.from_numpy(np.maximum(a, np.float32(1e-30)))
+
+
+def synth_bernoulli(shape: Tuple[int, ...], keep: float, seed: int) -> torch.Tensor:
+    """{0, 1} float32 samples with P(1) = keep -- recorded stochastic-depth masks."""
+    g = _rng(seed, "bern/" + "x".join(str(int(s)) for s in shape))
+    return torch.from_numpy((g.random(size=tuple(shape)) < keep).astype(np.float32))

@@ -38,6 +38,8 @@ extern "C" {
 #define PIPNET_EPI_MUL 4        /* C = (A W^T) * R          (BilinearIntermediate W(e)*V(e)) */
 #define PIPNET_EPI_BIAS_RELU 5  /* C = relu(A W^T + b)            (ResNet conv+BN+ReLU)      */
 #define PIPNET_EPI_BIAS_RESID_RELU 6 /* C = relu(A W^T + b + R) (Bottleneck conv3+BN+identity+ReLU) */
+#define PIPNET_EPI_RESID_ROWSCALE 7  /* C = R + rs[m/g] * (s * (A W^T + b))  (pipnet_linear_rowscale_f32:
+                                        CNBlock Linear2 with train-mode stochastic depth)              */
 
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -52,6 +54,14 @@ const char* pipnet_amd_status_string(int status);
 int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                       int M, int N, int K, int epilogue, void* stream);
+
+/* pipnet_linear_f32 with PIPNET_EPI_RESID_ROWSCALE: C = R + row_scale[m / rows_per_scale] *
+ * (scale * (A W^T + bias)).  The CNBlock's Linear2 * layer_scale + residual under
+ * torchvision's StochasticDepth("row") in train mode: rows_per_scale = H*W (one factor per
+ * sample), row_scale[b] = keep_b / (1 - p) -- 0 leaves a dropped sample's rows equal to R. */
+int pipnet_linear_rowscale_f32(const float* A, int64_t lda, const float* W, const float* bias, const float* scale,
+                               const float* R, int64_t ldr, float* C, int64_t ldc, int M, int N, int K,
+                               const float* row_scale, int rows_per_scale, void* stream);
 
 /* Split-K variant for short-M products (M <= a few hundred rows, long K: the Bilinear /
  * LinearFull intermediate GEMMs at M = batch, count_pipnet_utils.py:342-385): the K range
@@ -223,6 +233,40 @@ int pipnet_resize_normalize_rgb8(const uint8_t* pixels, const int64_t* offsets, 
                                  int B, int out_h, int out_w, int kmax, int grayscale,
                                  const float* mean3, const float* std3, int32_t* workspace,
                                  float* out, uint8_t* out_u8, void* stream);
+
+/* ---- training step, finetune phase (pipnet/train.py:75-140) ----
+ * The batch is cat([xs1, xs2]) (train.py:84): N = 2*Bh rows, proto features NHWC
+ * [N][HW][P] (rows n and Bh*HW + n are the two views of one pixel), pooled [N][P],
+ * out [N][K], ys int64 [Bh] (row r's label is ys[r % Bh], train.py:155).
+ *
+ * pipnet_train_align_partial_f32: align_loss (train.py:259-265) partial sums, one double
+ *   per workgroup into partial[pipnet_train_align_partials()].  P % 4 == 0 needs pf
+ *   16-byte aligned.
+ * pipnet_train_loss_f32 (train.py:154-250): stats[8] = {align, tanh, class, total loss,
+ *   correct count, w_align, w_tanh, w_class}; mode 0 train, 1 pretrain (no class term, no
+ *   d_out), 2 finetune (loss = w_class * class).  mult = normalization_multiplier (device
+ *   float[1]); enforce = enforce_weight_sparsity (class input log1p(out^mult)).
+ *   d_out [N][K] = d loss / d out (w_class * d class).
+ * pipnet_nonneg_linear_bwd_f32 (pipnet.py:54-71 backward): dW = (W > 0) * d_out^T x,
+ *   db = sum_r d_out (db may be NULL).  x [N][D], W/dW [K][D].
+ * pipnet_adamw_step_f32: torch.optim.AdamW on one tensor at optimizer step ``step`` (1-based),
+ *   hyper-parameters in double as torch's param_groups hold them (the float constants the
+ *   kernel uses -- 1 - lr*wd, 1 - beta1, 1 - beta2, lr/(1 - beta1^t), sqrt(1 - beta2^t) --
+ *   are derived from them in double, as torch does), then if post != 0
+ *   p = max(p - post_delta, post_floor) (train.py:134-140's clamps).
+ * pipnet_clamp_min_f32: x = max(x, lo) (normalization_multiplier clamp, train.py:137). */
+int pipnet_train_align_partials(void);
+int pipnet_train_align_partial_f32(const float* pf, int Bh, int HW, int P, double* partial, void* stream);
+int pipnet_train_loss_f32(const double* align_partial, int Bh, int HW, const float* pooled, const float* out,
+                          const int64_t* ys, int P, int K, const float* mult, int enforce, float tanh_coeff,
+                          float w_align, float w_tanh, float w_class, int mode, float* d_out, float* stats,
+                          void* stream);
+int pipnet_nonneg_linear_bwd_f32(const float* d_out, const float* x, int N, int D, const float* W, int K,
+                                 float* dW, float* db, void* stream);
+int pipnet_adamw_step_f32(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                          double lr, double beta1, double beta2, double eps, double weight_decay, int64_t step,
+                          int post, float post_delta, float post_floor, void* stream);
+int pipnet_clamp_min_f32(float* x, int64_t n, float lo, void* stream);
 
 #ifdef __cplusplus
 }

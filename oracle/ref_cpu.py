@@ -40,20 +40,35 @@ def downsample_stride(net: str, in_channels: int) -> int:
     return 1 if in_channels > threshold else 2
 
 
+SD_PROB = 0.1          # torchvision convnext_tiny(stochastic_depth_prob=0.1)
+N_BLOCKS = sum(n for _, _, n in CONVNEXT_TINY)
+
+
+def sd_drop_prob(bid: int) -> float:
+    """torchvision ConvNeXt: block ``bid`` (0..17 over all stages) drops its residual
+    branch with p = 0.1 * bid / 17 in train mode (StochasticDepth "row")."""
+    return SD_PROB * bid / (N_BLOCKS - 1.0)
+
+
 def convnext_features(x: Tensor, sd: SD, prefix: str, net: str = "convnext_tiny_26",
-                      use_mid_layers: bool = False, num_stages: int = 2) -> Tensor:
+                      use_mid_layers: bool = False, num_stages: int = 2,
+                      sd_keep: Optional[Dict[int, Tensor]] = None) -> Tensor:
     """features/convnext_features.py:38-94 (+ MidLayerConvNeXt :17-36) over the
-    torchvision ConvNeXt-tiny ``features`` Sequential."""
+    torchvision ConvNeXt-tiny ``features`` Sequential.  ``sd_keep`` =
+    train-mode stochastic depth: block id -> per-sample keep mask {0,1} [B] (blocks with
+    p > 0); the branch is scaled by mask / (1 - p) as torchvision's StochasticDepth does."""
     p = prefix + "features."
     # stem: Conv2d k4 s4 + LayerNorm2d  (features.0)
     x = F.conv2d(x, sd[p + "0.0.weight"], sd[p + "0.0.bias"], stride=4)
     x = _ln2d(x, sd[p + "0.1.weight"], sd[p + "0.1.bias"])
     last = 7 if not use_mid_layers else min(num_stages, 7)      # MidLayerConvNeXt :27-31
     idx = 1
+    bid = -1
     for cin, cout, n in CONVNEXT_TINY:
         if idx > last:
             break
         for j in range(n):                                       # CNBlock (torchvision)
+            bid += 1
             q = f"{p}{idx}.{j}."
             y = F.conv2d(x, sd[q + "block.0.weight"], sd[q + "block.0.bias"], padding=3, groups=cin)
             y = y.permute(0, 2, 3, 1)
@@ -62,7 +77,11 @@ def convnext_features(x: Tensor, sd: SD, prefix: str, net: str = "convnext_tiny_
             y = F.gelu(y)
             y = F.linear(y, sd[q + "block.5.weight"], sd[q + "block.5.bias"])
             y = y.permute(0, 3, 1, 2)
-            x = sd[q + "layer_scale"] * y + x
+            y = sd[q + "layer_scale"] * y
+            if sd_keep is not None and sd_drop_prob(bid) > 0.0:
+                keep = 1.0 - sd_drop_prob(bid)
+                y = y * (sd_keep[bid].to(y.dtype) / keep).view(-1, 1, 1, 1)
+            x = y + x
         idx += 1
         if cout is None or idx > last:
             break
@@ -151,10 +170,10 @@ def pipnet_forward_bf16(xs: Tensor, sd: SD, cfg, inference: bool = False) -> Tup
     return proto, pooled, out
 
 
-def backbone(x: Tensor, sd: SD, cfg) -> Tensor:
+def backbone(x: Tensor, sd: SD, cfg, sd_keep: Optional[Dict[int, Tensor]] = None) -> Tensor:
     if "convnext" in cfg.net:
         return convnext_features(x, sd, "_net.", cfg.net, getattr(cfg, "use_mid_layers", False),
-                                 getattr(cfg, "num_stages", 2))
+                                 getattr(cfg, "num_stages", 2), sd_keep)
     if cfg.net == "resnet50":
         return resnet50_features(x, sd, "_net.")
     raise ValueError(f"oracle: unsupported net {cfg.net}")
@@ -165,9 +184,11 @@ def non_neg_linear(x: Tensor, w: Tensor, b: Optional[Tensor]) -> Tensor:
     return F.linear(x, torch.relu(w), b)
 
 
-def pipnet_forward(xs: Tensor, sd: SD, cfg, inference: bool = False) -> Tuple[Tensor, Tensor, Tensor]:
-    """pipnet/pipnet.py:31-41 with the add-on / pool of get_pip_network :92-108."""
-    feats = backbone(xs, sd, cfg)
+def pipnet_forward(xs: Tensor, sd: SD, cfg, inference: bool = False,
+                   sd_keep: Optional[Dict[int, Tensor]] = None) -> Tuple[Tensor, Tensor, Tensor]:
+    """pipnet/pipnet.py:31-41 with the add-on / pool of get_pip_network :92-108
+    (``sd_keep``: train-mode stochastic depth masks, see convnext_features)."""
+    feats = backbone(xs, sd, cfg, sd_keep)
     if getattr(cfg, "num_features", 0):
         feats = F.conv2d(feats, sd["_add_on.0.weight"], sd["_add_on.0.bias"])
     proto = torch.softmax(feats, dim=1)                          # nn.Softmax(dim=1)

@@ -1,0 +1,173 @@
+"""Golden fixtures for the finetune-phase training iteration, recorded
+by running the REFERENCE's own ``pipnet/train.py:train_pipnet`` (unchanged) on CPU with
+``finetune=True`` for a few iterations.
+
+Setup mirrors main.py: the net of a forward golden case (gen_golden.CASES, same synthetic
+weights) in ``nn.DataParallel`` (CPU: calls the module directly), optimizers from the
+reference's ``util/args.py:get_optimizer_nn`` (AdamW; lr 0.05, weight decay 0.01 on the
+classifier weight), the finetune freeze of main.py:333-345 (only ``_classification``
+trains), ``CosineAnnealingWarmRestarts(T_0=10, eta_min=0.001)`` as main.py:314,
+``NLLLoss``, ``enforce_weight_sparsity=True``.
+
+Stochastic depth: ``torch.Tensor.bernoulli_`` is patched to emit ``synth_bernoulli``
+masks (recorded).  They are drawn with keep probability min(1 - p, 0.75) so that drops
+actually occur in a few-iteration fixture; the branch scale is still the module's own
+1/(1 - p), so the masks are simply an input of the step.
+
+Recorded per iteration i: labels, the SD masks (one per CNBlock with p > 0, in forward
+order), the forward's ``pooled`` / ``out`` (forward hook), the proto map (small cases),
+the classifier weight / bias / multiplier the forward saw, the loss components and
+accuracy ``calculate_loss`` returned; at the end: classifier weight / bias / multiplier,
+AdamW state and ``train_info``.
+
+Usage:  python tests/golden/gen_golden_train.py
+"""
+from __future__ import annotations
+
+import argparse
+import contextlib
+import io
+import json
+import os
+import sys
+
+sys.dont_write_bytecode = True            # /root/reference is read-only
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+import gen_golden as G  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(HERE))
+from golden_util import train_loader_batches  # noqa: E402
+from count_pipnet_amd.synthetic import synth_bernoulli  # noqa: E402
+
+# name -> (forward golden case, iterations, batch per view, seed, record proto map)
+TRAIN_CASES = {
+    "train_finetune_mid_addon": ("pipnet_mid_addon", 3, 3, 301, True),
+    "train_finetune_c2": ("c2_pipnet_convnext26", 2, 2, 302, False),
+}
+LR, WD = 0.05, 0.01
+
+
+@contextlib.contextmanager
+def injected_bernoulli(seed: int):
+    orig = torch.Tensor.bernoulli_
+    drawn = []
+
+    def fake(self, p=0.5, *, generator=None):
+        mask = synth_bernoulli(tuple(self.shape), min(float(p), 0.75), seed + len(drawn))
+        drawn.append(mask.flatten().clone())
+        with torch.no_grad():
+            self.copy_(mask)
+        return self
+
+    torch.Tensor.bernoulli_ = fake
+    try:
+        yield drawn
+    finally:
+        torch.Tensor.bernoulli_ = orig
+
+
+def run(name):
+    fwd_case, nb, bs, seed, keep_proto = TRAIN_CASES[name]
+    net, case = G.build_reference(fwd_case)
+    sys.path.insert(0, G.REF)
+    import pipnet.train as ref_train
+    from util.args import get_optimizer_nn
+    dp = nn.DataParallel(net)
+    args = argparse.Namespace(net=case["net"], use_mid_layers=case.get("use_mid_layers", False),
+                              num_stages=case.get("num_stages", 2), bias=case["bias"], lr=LR, lr_net=5e-4,
+                              lr_block=5e-4, weight_decay=WD, optimizer="Adam", seed=1, train_intermediate=False)
+    with contextlib.redirect_stdout(io.StringIO()):
+        opt_net, opt_cls, _, _, _ = get_optimizer_nn(dp, args)
+    for p in net.parameters():                       # main.py:335-339 (finetune)
+        p.requires_grad = False
+    for p in net._classification.parameters():
+        p.requires_grad = True
+    net._classification.normalization_multiplier.requires_grad = False
+    sched_net = torch.optim.lr_scheduler.CosineAnnealingLR(opt_net, T_max=10, eta_min=5e-6)
+    sched_cls = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt_cls, T_0=10, eta_min=0.001, T_mult=1)
+    criterion = nn.NLLLoss(reduction="mean")
+    batches = train_loader_batches(case["size"], case["num_classes"], nb, bs, seed)
+
+    seen, comps = [], []
+
+    def hook(mod, inp, outp):
+        cls = mod._classification
+        seen.append(dict(pooled=outp[1].detach().clone(), out=outp[2].detach().clone(),
+                         proto=outp[0].detach().clone() if keep_proto else None,
+                         w=cls.weight.detach().clone(),
+                         b=None if cls.bias is None else cls.bias.detach().clone(),
+                         mult=cls.normalization_multiplier.detach().clone()))
+
+    orig_loss = ref_train.calculate_loss
+
+    def rec_loss(*a, **kw):
+        loss, acc, comp = orig_loss(*a, **kw)
+        comps.append(dict(comp, acc=acc, loss=float(loss.item())))
+        return loss, acc, comp
+
+    ref_train.calculate_loss = rec_loss
+    h = net.register_forward_hook(hook)
+    try:
+        with injected_bernoulli(seed=5000 + seed) as drawn, contextlib.redirect_stdout(io.StringIO()), \
+                contextlib.redirect_stderr(io.StringIO()):
+            info = ref_train.train_pipnet(dp, batches, opt_net, opt_cls, sched_net, sched_cls, criterion, 1, 1,
+                                          torch.device("cpu"), is_count_pipnet=False, pretrain=False,
+                                          finetune=True, enforce_weight_sparsity=True)
+    finally:
+        h.remove()
+        ref_train.calculate_loss = orig_loss
+    nmask = len(drawn) // nb
+    rec = {}
+
+    def put(key, t):
+        """Full tensors for small cases; for the C2-sized head: first 8 rows + row sums."""
+        a = t.detach().numpy()
+        if keep_proto or a.ndim < 2:
+            rec[key] = a
+        else:
+            rec[key + "_rows8"] = a[:8]
+            rec[key + "_rowsum"] = a.astype(np.float64).sum(axis=1)
+    for i, ((xs1, xs2, ys), s) in enumerate(zip(batches, seen)):
+        rec[f"s{i}_ys"] = ys.numpy()
+        rec[f"s{i}_masks"] = torch.stack(drawn[i * nmask:(i + 1) * nmask]).numpy()
+        for k in ("pooled", "out", "b", "mult", "proto"):
+            if s[k] is not None:
+                rec[f"s{i}_{k}"] = s[k].numpy()
+        if keep_proto:
+            rec[f"s{i}_w"] = s["w"].numpy()
+    cls = net._classification
+    put("final_w", cls.weight)
+    rec["final_mult"] = cls.normalization_multiplier.detach().numpy()
+    st = opt_cls.state[cls.weight]
+    put("final_w_exp_avg", st["exp_avg"])
+    put("final_w_exp_avg_sq", st["exp_avg_sq"])
+    if cls.bias is not None:
+        rec["final_b"] = cls.bias.detach().numpy()
+        rec["final_b_exp_avg"] = opt_cls.state[cls.bias]["exp_avg"].numpy()
+        rec["final_b_exp_avg_sq"] = opt_cls.state[cls.bias]["exp_avg_sq"].numpy()
+    meta = dict(name=name, forward_case=fwd_case, iterations=nb, batch_per_view=bs, seed=seed,
+                mask_seed=5000 + seed, masks_per_step=nmask, lr=LR, weight_decay=WD,
+                steps=float(st["step"]), components=comps,
+                info={k: (v if isinstance(v, list) else float(v)) for k, v in info.items()},
+                torch=torch.__version__)
+    rec["meta"] = np.array(json.dumps(meta))
+    return rec
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 8)
+    for name in TRAIN_CASES:
+        rec = run(name)
+        path = os.path.join(HERE, f"{name}.npz")
+        np.savez_compressed(path, **rec)
+        meta = json.loads(str(rec["meta"]))
+        print(f"wrote {path} ({os.path.getsize(path) / 1e3:.1f} kB)", meta["components"], flush=True)
+
+
+if __name__ == "__main__":
+    main()

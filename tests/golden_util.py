@@ -15,9 +15,10 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def golden_names():
     """Forward golden cases (eval_* fixtures belong to the eval_pipnet metric loop, input_*
-    to the input transform, tests/test_input_oracle.py)."""
+    to the input transform, tests/test_input_oracle.py, train_* to the finetune iteration,
+    tests/test_train_oracle.py)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR)
-                  if f.endswith(".npz") and not f.startswith(("eval_", "input_")))
+                  if f.endswith(".npz") and not f.startswith(("eval_", "input_", "train_")))
 
 
 def eval_golden_names():
@@ -73,3 +74,33 @@ def eval_loader_batches(size: int, num_classes: int, nb: int, bs: int, label_see
         ys = torch.randint(0, num_classes, (bs,), generator=g)
         out.append((xs, ys))
     return out
+
+
+def train_loader_batches(size: int, num_classes: int, nb: int, bs: int, seed: int):
+    """The in-memory loader of the train_* fixtures (tests/golden/gen_golden_train.py):
+    nb batches of (view-1 images, view-2 images, seeded labels)."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for i in range(nb):
+        xs1 = synth_images(bs, size, seed=seed * 100 + 2 * i)
+        xs2 = synth_images(bs, size, seed=seed * 100 + 2 * i + 1)
+        ys = torch.randint(0, num_classes, (bs,), generator=g)
+        out.append((xs1, xs2, ys))
+    return out
+
+
+def train_golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR) if f.startswith("train_") and f.endswith(".npz"))
+
+
+def load_train_golden(name: str):
+    """(train meta, arrays, forward-case meta) of a train_* fixture."""
+    meta, rec = load_golden(name)
+    fwd_meta, _ = load_golden(meta["forward_case"])
+    return meta, rec, fwd_meta
+
+
+def train_step_lrs(meta):
+    """Learning rate each iteration's optimizer step used: the initial lr, then the value
+    the scheduler set after the previous iteration (train.py:120-122)."""
+    return [meta["lr"]] + meta["info"]["lrs_class"][:-1]

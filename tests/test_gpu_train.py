@@ -1,0 +1,240 @@
+"""Finetune-phase training iteration on the GPU (csrc/train_ops.hip, count_pipnet_amd.train).
+
+* loss kernel on the reference's recorded forward outputs == the reference's loss terms
+  (tests/golden/train_*.npz) and == the oracle; d loss / d out == the oracle's explicit
+  derivative; larger random shapes (C2 head size) against the oracle in float64;
+* NonNegLinear backward == oracle; AdamW kernel == torch.optim.AdamW;
+* end to end: count_pipnet_amd.train on the HIP model with the reference's weights, images,
+  labels and recorded stochastic-depth masks reproduces the reference's loss terms and its
+  classifier / AdamW state after every iteration (fp32 forward parity ~1e-5 feeds Adam's
+  sign-like first steps, so weights are compared elementwise with a 99 % quorum);
+* the HIP forward in train mode (stochastic depth) == the oracle forward with the same masks.
+"""
+import contextlib
+import io
+
+import numpy as np
+import pytest
+import torch
+
+from count_pipnet_amd import kernels as K
+from count_pipnet_amd import train as T
+from count_pipnet_amd.convnext_features import CNBlock
+from golden_util import load_train_golden, train_golden_names, train_loader_batches, train_step_lrs
+from model_util import build_model
+from oracle import ref_cpu, train_ref
+
+pytestmark = pytest.mark.gpu
+NAMES = train_golden_names()
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a))
+
+
+def _nhwc(proto_nchw):
+    return proto_nchw.permute(0, 2, 3, 1).contiguous()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_loss_kernel_matches_reference(gpu, name):
+    meta, rec, _ = load_train_golden(name)
+    for i, comp in enumerate(meta["components"]):
+        pooled, out, ys = _t(rec[f"s{i}_pooled"]), _t(rec[f"s{i}_out"]), _t(rec[f"s{i}_ys"])
+        mult = _t(rec[f"s{i}_mult"])
+        if f"s{i}_proto" in rec:
+            proto = _t(rec[f"s{i}_proto"])
+        else:   # C2 fixture has no proto map: a synthetic softmax map (align checked vs the oracle)
+            g = torch.Generator().manual_seed(i)
+            proto = torch.softmax(torch.randn(pooled.shape[0], pooled.shape[1], 5, 7, generator=g) * 3, dim=1)
+        stats, d_out = K.train_loss(_nhwc(proto).to(gpu), pooled.to(gpu), out.to(gpu), ys.to(gpu), mult.to(gpu),
+                                    True, 1.0, 5.0, 2.0, 2.0, "finetune")
+        s = stats.cpu()
+        ref = train_ref.loss_terms(proto, pooled, out, ys, float(mult[0]))
+        assert float(s[1]) == pytest.approx(comp["tanh"], rel=1e-5, abs=1e-6)
+        assert float(s[2]) == pytest.approx(comp["class"], rel=1e-5, abs=1e-6)
+        assert float(s[3]) == pytest.approx(comp["loss"], rel=1e-5, abs=1e-6)
+        assert float(s[4]) / (2 * len(ys)) == comp["acc"]
+        assert float(s[0]) == pytest.approx(float(ref["align"]), rel=1e-5, abs=1e-6)
+        if f"s{i}_proto" in rec:
+            assert float(s[0]) == pytest.approx(comp["align"], rel=1e-5, abs=1e-6)
+        torch.testing.assert_close(d_out.cpu(), train_ref.d_out(out, ys, float(mult[0]), True, 2.0),
+                                   rtol=1e-5, atol=1e-8)
+
+
+@pytest.mark.parametrize("bh,hw,p,k,mult,enforce", [(64, 676, 768, 200, 1.0, True), (4, 9, 30, 7, 2.0, True),
+                                                     (3, 16, 64, 10, 1.5, False), (2, 1, 4, 3, 1.0, True)])
+def test_loss_kernel_random_shapes(gpu, bh, hw, p, k, mult, enforce):
+    g = torch.Generator().manual_seed(bh * 1000 + p)
+    n = 2 * bh
+    logits = torch.randn(n, p, hw, generator=g) * 2
+    proto = torch.softmax(logits, dim=1).view(n, p, hw, 1)
+    pooled = proto.amax(dim=(2, 3))
+    w = torch.relu(torch.randn(k, p, generator=g))
+    out = pooled @ w.t()
+    ys = torch.randint(0, k, (bh,), generator=g)
+    mt = torch.tensor([mult])
+    for mode in ("finetune", "train", "pretrain"):
+        stats, d_out = K.train_loss(_nhwc(proto).to(gpu), pooled.to(gpu), out.to(gpu), ys.to(gpu), mt.to(gpu),
+                                    enforce, 1.0, 5.0, 2.0, 2.0, mode)
+        s = stats.cpu().double()
+        ref = train_ref.loss_terms(proto.double(), pooled.double(), out.double(), ys, mult, enforce)
+        assert float(s[0]) == pytest.approx(float(ref["align"]), rel=2e-5, abs=1e-6)
+        assert float(s[1]) == pytest.approx(float(ref["tanh"]), rel=2e-5, abs=1e-6)
+        assert float(s[2]) == pytest.approx(float(ref["cls"]), rel=2e-5, abs=1e-6)
+        assert float(s[4]) == float(ref["correct"])
+        want = {"finetune": 2.0 * ref["cls"], "train": 5.0 * ref["align"] + 2.0 * ref["tanh"] + 2.0 * ref["cls"],
+                "pretrain": 5.0 * ref["align"] + 2.0 * ref["tanh"]}[mode]
+        assert float(s[3]) == pytest.approx(float(want), rel=2e-5, abs=1e-6)
+        if mode == "pretrain":
+            assert d_out is None
+        else:
+            torch.testing.assert_close(d_out.cpu().double(), train_ref.d_out(out.double(), ys, mult, enforce, 2.0),
+                                       rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,d,k", [(128, 768, 200), (6, 32, 10), (5, 37, 3)])
+def test_nonneg_linear_backward(gpu, n, d, k):
+    g = torch.Generator().manual_seed(n + d + k)
+    d_out = torch.randn(n, k, generator=g) * 1e-2
+    x = torch.rand(n, d, generator=g)
+    w = torch.randn(k, d, generator=g)
+    w[w.abs() < 0.3] = 0.0
+    dw, db = K.nonneg_linear_backward(d_out.to(gpu), x.to(gpu), w.to(gpu), True)
+    rw, rb = train_ref.nonneg_linear_grads(d_out.double(), x.double(), w.double())
+    torch.testing.assert_close(dw.cpu().double(), rw, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(db.cpu().double(), rb, rtol=1e-5, atol=1e-7)
+    assert torch.all(dw.cpu()[w <= 0] == 0)
+
+
+@pytest.mark.parametrize("post", [None, (1e-3, 0.0), (0.0, 0.0)])
+def test_adamw_kernel_matches_torch(gpu, post):
+    g = torch.Generator().manual_seed(7)
+    p0 = torch.randn(200, 768, generator=g)
+    p = p0.clone().to(gpu).requires_grad_(True)
+    opt = torch.optim.AdamW([p], lr=0.05, weight_decay=0.01)
+    q = p0.clone().to(gpu)
+    m, v = torch.zeros_like(q), torch.zeros_like(q)
+    for step in range(1, 5):
+        grad = (torch.randn(200, 768, generator=g) * 10 ** (-step)).to(gpu)
+        p.grad = grad.clone()
+        opt.step()
+        if post is not None:
+            with torch.no_grad():
+                p.copy_(torch.clamp(p - post[0], min=post[1]))
+        K.adamw_step_(q, grad, m, v, 0.05, 0.9, 0.999, 1e-8, 0.01, step, post)
+        # within an ulp or two of each operand's scale: torch's foreach AdamW rounds v * beta2,
+        # p * (1 - lr * wd) and lerp's product in separate kernels, the fused kernel may
+        # contract them into FMAs (m = m + w (g - m) then differs by ~1 ulp of w g, which is
+        # large relative to m only where m nearly cancels)
+        ms = opt.state[p]["exp_avg"].abs().max().item()
+        vs = opt.state[p]["exp_avg_sq"].abs().max().item()
+        torch.testing.assert_close(q, p.detach(), rtol=1e-6, atol=3e-7)
+        torch.testing.assert_close(m, opt.state[p]["exp_avg"], rtol=1e-6, atol=1e-6 * ms)
+        torch.testing.assert_close(v, opt.state[p]["exp_avg_sq"], rtol=1e-6, atol=1e-6 * vs)
+
+
+def _finetune_setup(name, gpu):
+    meta, rec, fwd_meta = load_train_golden(name)
+    net = build_model(fwd_meta).to(gpu).train()
+    for prm in net.parameters():
+        prm.requires_grad = False
+    for prm in net._classification.parameters():
+        prm.requires_grad = True
+    net._classification.normalization_multiplier.requires_grad = False
+    cls = net._classification
+    groups = [{"params": [cls.weight], "lr": meta["lr"], "weight_decay": meta["weight_decay"]}]
+    if cls.bias is not None:
+        groups.append({"params": [cls.bias], "lr": meta["lr"], "weight_decay": 0.0})
+    opt = torch.optim.AdamW(groups, lr=meta["lr"], weight_decay=0.0)
+    sched = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt, T_0=10, eta_min=0.001, T_mult=1)
+    c = fwd_meta["case"]
+    batches = train_loader_batches(c["size"], c["num_classes"], meta["iterations"], meta["batch_per_view"],
+                                   meta["seed"])
+    return meta, rec, fwd_meta, net, opt, sched, batches
+
+
+def _sd_keep(net, masks):
+    """Recorded masks (forward order of the blocks with p > 0) -> {block id: bool mask}."""
+    blocks = [m for m in net._net.features.modules() if isinstance(m, CNBlock)]
+    ids = [bid for bid, b in enumerate(blocks) if b.stochastic_depth.p > 0.0]
+    assert len(ids) == masks.shape[0]
+    return {bid: _t(masks[j]) > 0.5 for j, bid in enumerate(ids)}
+
+
+def _quorum_close(a, b, rtol, atol, frac=0.99, max_abs=None):
+    a, b = a.detach().cpu().double(), b.detach().cpu().double()
+    ok = (a - b).abs() <= atol + rtol * b.abs()
+    assert ok.float().mean().item() >= frac, f"{(~ok).sum().item()} / {ok.numel()} elements differ"
+    if max_abs is not None:
+        assert (a - b).abs().max().item() <= max_abs
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_finetune_iterations_match_reference(gpu, name):
+    meta, rec, fwd_meta, net, opt, sched, batches = _finetune_setup(name, gpu)
+    cls = net._classification
+    iters = len(batches)
+    lr_max = meta["lr"]
+    for i, (xs1, xs2, ys) in enumerate(batches):
+        if f"s{i}_w" in rec:      # the weights this iteration's forward saw
+            _quorum_close(cls.weight, _t(rec[f"s{i}_w"]), 1e-4, 1e-5, max_abs=4 * lr_max * i + 1e-6)
+        sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
+        proto, pooled, out = T.train_forward_hip(net, torch.cat([xs1, xs2]).to(gpu), sd_keep)
+        torch.testing.assert_close(pooled.cpu(), _t(rec[f"s{i}_pooled"]), rtol=1e-3, atol=2e-4)
+        torch.testing.assert_close(out.cpu(), _t(rec[f"s{i}_out"]), rtol=1e-3, atol=2e-3)
+        opt.zero_grad(set_to_none=True)
+        stats = T.hip_finetune_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt, True, sd_keep=sd_keep).cpu()
+        comp = meta["components"][i]
+        assert float(stats[2]) == pytest.approx(comp["class"], rel=1e-3, abs=1e-4)
+        assert float(stats[1]) == pytest.approx(comp["tanh"], rel=1e-3, abs=1e-4)
+        assert float(stats[0]) == pytest.approx(comp["align"], rel=1e-3, abs=1e-4)
+        assert float(stats[3]) == pytest.approx(comp["loss"], rel=1e-3, abs=1e-4)
+        sched.step(0 + i / iters)
+    assert [pytest.approx(x) for x in meta["info"]["lrs_class"][-1:]] == [sched.get_last_lr()[0]]
+    bound = 4 * lr_max * iters + 1e-6
+    st = opt.state[cls.weight]
+    assert float(st["step"]) == meta["steps"]
+    if "final_w" in rec:
+        _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, max_abs=bound)
+        _quorum_close(st["exp_avg"], _t(rec["final_w_exp_avg"]), 1e-3, 1e-7)
+        _quorum_close(st["exp_avg_sq"], _t(rec["final_w_exp_avg_sq"]), 1e-3, 1e-10)
+    else:
+        _quorum_close(cls.weight[:8], _t(rec["final_w_rows8"]), 1e-4, 1e-5, max_abs=bound)
+        _quorum_close(st["exp_avg"][:8], _t(rec["final_w_exp_avg_rows8"]), 1e-3, 1e-7)
+    if cls.bias is not None:
+        _quorum_close(cls.bias, _t(rec["final_b"]), 1e-4, 1e-5, frac=0.9, max_abs=bound)
+    assert float(cls.normalization_multiplier[0]) == pytest.approx(float(rec["final_mult"][0]))
+
+
+def test_train_pipnet_epoch(gpu):
+    name = NAMES[0]
+    meta, rec, fwd_meta, net, opt, sched, batches = _finetune_setup(name, gpu)
+    with contextlib.redirect_stdout(io.StringIO()):
+        info = T.train_pipnet(net, batches, opt, opt, None, sched, None, 1, 1, gpu, finetune=True,
+                              generator=torch.Generator().manual_seed(0))
+    for k in ("align_loss_raw", "tanh_loss_raw", "class_loss_raw", "align_loss_weighted", "tanh_loss_weighted",
+              "class_loss_weighted", "train_accuracy", "loss", "lrs_net", "lrs_class"):
+        assert k in info
+    assert info["lrs_class"] == pytest.approx(meta["info"]["lrs_class"])
+    assert info["loss"] == pytest.approx(2.0 * info["class_loss_raw"], rel=1e-5)
+    assert np.isfinite(info["loss"]) and 0.0 <= info["train_accuracy"] <= 1.0
+    assert info["class_loss_raw"] == pytest.approx(meta["info"]["class_loss_raw"], rel=0.1)
+
+
+def test_train_forward_stochastic_depth_matches_oracle(gpu):
+    """Full ConvNeXt-26 at 224 with drops in most blocks: the HIP train-mode forward (dropped
+    samples skip the branch) == the oracle forward scaling the branch by mask / (1 - p)."""
+    meta, rec, fwd_meta = load_train_golden("train_finetune_c2")
+    net = build_model(fwd_meta).to(gpu).train()
+    g = torch.Generator().manual_seed(3)
+    xs = torch.randn(6, 3, 224, 224, generator=g)
+    masks = T.stochastic_depth_masks(net._net.features, 6, g)
+    masks = {b: m & (torch.rand(6, generator=g) < 0.7) for b, m in masks.items()}   # force drops
+    proto, pooled, out = T.train_forward_hip(net, xs.to(gpu), masks)
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    from golden_util import golden_args
+    rp, rpool, rout = ref_cpu.pipnet_forward(xs, sd, golden_args(fwd_meta), inference=False, sd_keep=masks)
+    torch.testing.assert_close(pooled.cpu(), rpool, rtol=1e-3, atol=2e-4)
+    torch.testing.assert_close(out.cpu(), rout, rtol=1e-3, atol=2e-3)
+    torch.testing.assert_close(proto.cpu().permute(0, 3, 1, 2), rp, rtol=1e-3, atol=2e-4)
