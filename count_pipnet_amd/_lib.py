@@ -55,8 +55,13 @@ SIGNATURES = {
     "pipnet_nonneg_linear_bwd_f32": [P, P, I32, I32, P, I32, P, P, P],
     "pipnet_adamw_step_f32": [P, P, P, P, I64, F64, F64, F64, F64, F64, I64, I32, F32, F32, P],
     "pipnet_clamp_min_f32": [P, I64, F32, P],
+    "pipnet_wgrad_workspace_bytes": [I32, I32, I32],
+    "pipnet_wgrad_f32": [P, I64, P, I64, I32, I32, I32, P, I64, I32, P, P],
+    "pipnet_colsum_workspace_bytes": [I32],
+    "pipnet_colsum_f32": [P, I64, I32, I32, P, I32, P, P],
 }
-_RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p}
+_RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64}
+_RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, **_RESTYPE_EXTRA}
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
 EPI_RESID_ROWSCALE = 7

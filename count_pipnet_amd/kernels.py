@@ -550,3 +550,39 @@ def clamp_min_(x: Tensor, lo: float) -> Tensor:
     _chk(x, "tensor")
     _lib.call("pipnet_clamp_min_f32", x.data_ptr(), x.numel(), lo, _stream(x))
     return x
+
+
+# ---- backward building blocks (csrc/backward_ops.hip) ----------------------------------------
+def wgrad(a: Tensor, b: Tensor, out: Optional[Tensor] = None, accumulate: bool = False) -> Tensor:
+    """out[N1,N2] (+)= a[M,N1]^T @ b[M,N2] (weight gradient dY^T X), deterministic."""
+    for t, what in ((a, "wgrad A"), (b, "wgrad B")):
+        require_device(t, what)
+        if t.dim() != 2 or t.stride(1) != 1:
+            raise RuntimeError(f"{what}: expects a 2-D row-major view")
+    m, n1 = a.shape
+    if b.shape[0] != m:
+        raise RuntimeError(f"wgrad: row counts differ {tuple(a.shape)} vs {tuple(b.shape)}")
+    n2 = b.shape[1]
+    if out is None:
+        if accumulate:
+            raise RuntimeError("wgrad: accumulate needs out")
+        out = torch.empty((n1, n2), device=a.device, dtype=torch.float32)
+    elif tuple(out.shape) != (n1, n2) or out.stride(1) != 1:
+        raise RuntimeError("wgrad: out shape")
+    nbytes = _lib.load().pipnet_wgrad_workspace_bytes(m, n1, n2)
+    ws = torch.empty(max(nbytes // 4, 1), device=a.device, dtype=torch.float32)
+    _lib.call("pipnet_wgrad_f32", a.data_ptr(), a.stride(0), b.data_ptr(), b.stride(0), m, n1, n2, out.data_ptr(),
+              out.stride(0), int(accumulate), ws.data_ptr(), _stream(a))
+    return out
+
+
+def colsum(a: Tensor, out: Optional[Tensor] = None, accumulate: bool = False) -> Tensor:
+    """out[N] (+)= a[M,N].sum(0), deterministic."""
+    require_device(a, "colsum input")
+    m, n = a.shape
+    if out is None:
+        out = torch.empty(n, device=a.device, dtype=torch.float32)
+    ws = torch.empty(_lib.load().pipnet_colsum_workspace_bytes(n) // 4, device=a.device, dtype=torch.float32)
+    _lib.call("pipnet_colsum_f32", a.data_ptr(), a.stride(0), m, n, out.data_ptr(), int(accumulate), ws.data_ptr(),
+              _stream(a))
+    return out

@@ -268,6 +268,22 @@ int pipnet_adamw_step_f32(float* param, const float* grad, float* exp_avg, float
                           int post, float post_delta, float post_floor, void* stream);
 int pipnet_clamp_min_f32(float* x, int64_t n, float lo, void* stream);
 
+/* ---- backward building blocks (trainable ConvNeXt stages) ----
+ * pipnet_wgrad_f32: C[N1][N2] (ldc) = (accumulate ? C : 0) + sum_m A[m][n1] B[m][n2]
+ *   (A [M][N1] lda, B [M][N2] ldb, both pixel-major as the forward stores activations):
+ *   the weight gradient dW = dY^T X of a Linear / 1x1 conv.  fp32 MFMA, deterministic
+ *   (fixed pixel slabs, fixed-order reduction).  N1, N2, lda, ldb % 4 == 0, A/B 16-B
+ *   aligned; workspace: pipnet_wgrad_workspace_bytes(M, N1, N2) bytes (needed unless the
+ *   call runs as a single slab without accumulate; pass it whenever that size is > 0).
+ * pipnet_colsum_f32: out[n] = (accumulate ? out[n] : 0) + sum_m A[m][n] (bias gradients);
+ *   workspace of pipnet_colsum_workspace_bytes(N) bytes. */
+int64_t pipnet_wgrad_workspace_bytes(int M, int N1, int N2);
+int pipnet_wgrad_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int M, int N1, int N2, float* C,
+                     int64_t ldc, int accumulate, float* workspace, void* stream);
+int pipnet_colsum_workspace_bytes(int N);
+int pipnet_colsum_f32(const float* A, int64_t lda, int M, int N, float* out, int accumulate, float* workspace,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))
 
 def declared_symbols():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(pipnet_\w+)\s*\(", txt, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(pipnet_\w+)\s*\(", txt, flags=re.M)))
 
 
 def test_header_declares_entry_points():
