@@ -57,14 +57,24 @@ SIGNATURES = {
     "pipnet_clamp_min_f32": [P, I64, F32, P],
     "pipnet_wgrad_workspace_bytes": [I32, I32, I32],
     "pipnet_wgrad_f32": [P, I64, P, I64, I32, I32, I32, P, I64, I32, P, P],
+    "pipnet_wgrad_conv2x2_f32": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P, P],
     "pipnet_colsum_workspace_bytes": [I32],
     "pipnet_colsum_f32": [P, I64, I32, I32, P, I32, P, P],
+    "pipnet_train_partials_floats": [I32],
+    "pipnet_gelu_fwd_f32": [P, P, I64, P],
+    "pipnet_resid_scale_f32": [P, P, P, P, I32, I64, I32, P, P],
+    "pipnet_ls_bwd_f32": [P, P, P, P, I32, I64, I32, P, P, P, I32, P, P],
+    "pipnet_ln_bwd_f32": [P, P, P, I64, I32, P, P, P, I32, P, P],
+    "pipnet_dwconv7_plain_f32": [P, I32, I32, I32, I32, P, P, I32, P, P],
+    "pipnet_dwconv7_wgrad_f32": [P, P, I32, I32, I32, I32, P, P, I32, P, P],
+    "pipnet_head_bwd_f32": [P, P, I32, I32, I32, P, P, I32, F32, F32, F32, P, P, P, P],
 }
-_RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64}
+_RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64}
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, **_RESTYPE_EXTRA}
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
 EPI_RESID_ROWSCALE = 7
+EPI_GELU_BWD = 8
 
 _lib = None
 

@@ -75,6 +75,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
     PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RELU)
     PIPNET_EPI_CASE(PIPNET_EPI_BIAS_RESID_RELU)
     PIPNET_EPI_CASE(PIPNET_EPI_RESID_ROWSCALE)
+    PIPNET_EPI_CASE(PIPNET_EPI_GELU_BWD)
     default: return PIPNET_ERR_ARG;
   }
 #undef PIPNET_EPI_CASE
@@ -89,10 +90,12 @@ extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, co
                                  int M, int N, int K, int epilogue, void* stream) {
   if (M < 0 || N < 0 || K <= 0) return PIPNET_ERR_ARG;
   if (M == 0 || N == 0) return PIPNET_OK;
-  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_BIAS_RESID_RELU) return PIPNET_ERR_ARG;
+  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_GELU_BWD || epilogue == PIPNET_EPI_RESID_ROWSCALE)
+    return PIPNET_ERR_ARG;
   if ((K & 3) || (lda & 3) || lda < K || ldc < N) return PIPNET_ERR_ARG;
   if (!A || !W || !C) return PIPNET_ERR_ARG;
-  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU) &&
+  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU ||
+       epilogue == PIPNET_EPI_GELU_BWD) &&
       (!R || ldr < N))
     return PIPNET_ERR_ARG;
   if (!aligned16(A) || !aligned16(W)) return PIPNET_ERR_ALIGN;
@@ -169,9 +172,10 @@ extern "C" int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float
   if (M < 0 || N <= 0 || K <= 0 || (N & 3) || (K % 32) || (lda & 3) || lda < K || (ldc & 3) || ldc < N)
     return PIPNET_ERR_ARG;
   if (splits > K / 32 || splits > 64 || !workspace || !A || !W || !C) return PIPNET_ERR_ARG;
-  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_BIAS_RESID_RELU)
+  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_GELU_BWD || epilogue == PIPNET_EPI_RESID_ROWSCALE)
     return PIPNET_ERR_ARG;
-  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU) &&
+  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU ||
+       epilogue == PIPNET_EPI_GELU_BWD) &&
       (!R || ldr < N || (ldr & 3) || !aligned16(R)))
     return PIPNET_ERR_ARG;
   if (!aligned16(A) || !aligned16(W) || !aligned16(C) || !aligned16(workspace) || (bias && !aligned16(bias)) ||
@@ -204,6 +208,7 @@ extern "C" int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float
     PIPNET_RED(PIPNET_EPI_MUL)
     PIPNET_RED(PIPNET_EPI_BIAS_RELU)
     PIPNET_RED(PIPNET_EPI_BIAS_RESID_RELU)
+    PIPNET_RED(PIPNET_EPI_GELU_BWD)
     default: return PIPNET_ERR_ARG;
   }
 #undef PIPNET_RED

@@ -142,6 +142,13 @@ PIPNET_DEV float gelu_fast(float x) {
   return x * (x < 0.f ? half_erfc : 1.0f - half_erfc);
 }
 
+// d gelu_erf(x) / dx = Phi(x) + x phi(x)  (training backward, EPI_GELU_BWD)
+PIPNET_DEV float gelu_grad(float x) {
+  const float cdf = 0.5f * erfcf(-x * 0.70710678118654752440f);
+  const float pdf = 0.39894228040143267794f * expf(-0.5f * x * x);
+  return fmaf(x, pdf, cdf);
+}
+
 // GELU by Abramowitz & Stegun 7.1.26 (|erf error| < 1.5e-7, GELU error < 2.2e-7 absolute, checked on [-8, 8])
 // on packed fp32 pairs: the polynomial, scaling and select run as v_pk_{fma,mul,add}_f32
 // (two lanes' worth per instruction), only rcp / exp2 are per element: ~8 VALU issues per
@@ -201,7 +208,7 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
     const int n = n0 + wn * 64 + j * 32 + lr;
     if (n >= p.N) continue;
     float bn = 0.f, sn = 1.f;
-    if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL) bn = p.bias ? p.bias[n] : 0.f;
+    if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && EPI != PIPNET_EPI_GELU_BWD) bn = p.bias ? p.bias[n] : 0.f;
     if (EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) sn = p.scale ? p.scale[n] : 1.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -215,6 +222,7 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
         if (EPI == PIPNET_EPI_RESID) x = p.R[(int64_t)m * p.ldr + n] + sn * (x + bn);
         if (EPI == PIPNET_EPI_RESID_ROWSCALE)
           x = p.R[(int64_t)m * p.ldr + n] + p.row_scale[m / p.rows_per_scale] * (sn * (x + bn));
+        if (EPI == PIPNET_EPI_GELU_BWD) x = x * gelu_grad(p.R[(int64_t)m * p.ldr + n]);
         if (EPI == PIPNET_EPI_MUL) x = x * p.R[(int64_t)m * p.ldr + n];
         if (EPI == PIPNET_EPI_BIAS_RELU) x = fmaxf(x + bn, 0.f);
         if (EPI == PIPNET_EPI_BIAS_RESID_RELU) x = fmaxf(x + bn + p.R[(int64_t)m * p.ldr + n], 0.f);
@@ -241,6 +249,10 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
   }
   if (EPI == PIPNET_EPI_RESID) x = r + sn * (x + bn);
   if (EPI == PIPNET_EPI_RESID_ROWSCALE) x = r + rs * (sn * (x + bn));   // (ls * y) * (mask / keep) + x
+  if (EPI == PIPNET_EPI_GELU_BWD) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = x[e] * gelu_grad(r[e]);
+  }
   if (EPI == PIPNET_EPI_MUL) x = x * r;
   if (EPI == PIPNET_EPI_BIAS_RELU) {
     x = x + bn;
@@ -266,14 +278,15 @@ template <int EPI, int TM>
 PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, int m0, int n0, int wm, int wn,
                              int lane, int wid) {
   constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU ||
-                         EPI == PIPNET_EPI_RESID_ROWSCALE;
+                         EPI == PIPNET_EPI_RESID_ROWSCALE || EPI == PIPNET_EPI_GELU_BWD;
   float* wt = smem + wid * 32 * 64;
   const int lr = lane & 31, lh = lane >> 5;
   const int c4 = lane & 15;
   const int n = n0 + wn * 64 + 4 * c4;
   const bool nok = n < p.N;
   f32x4 bn = {0.f, 0.f, 0.f, 0.f}, sn = {1.f, 1.f, 1.f, 1.f};
-  if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && p.bias && nok) bn = ld4(p.bias + n);   // (incl. lab GELU)
+  if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && EPI != PIPNET_EPI_GELU_BWD && p.bias && nok)
+    bn = ld4(p.bias + n);   // (incl. lab GELU)
   if ((EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) && p.scale && nok) sn = ld4(p.scale + n);
   f32x4 r[TM][8];
   if (HAS_R) {

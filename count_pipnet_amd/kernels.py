@@ -586,3 +586,95 @@ def colsum(a: Tensor, out: Optional[Tensor] = None, accumulate: bool = False) ->
     _lib.call("pipnet_colsum_f32", a.data_ptr(), a.stride(0), m, n, out.data_ptr(), int(accumulate), ws.data_ptr(),
               _stream(a))
     return out
+
+
+def _partials(c: int, device) -> Tensor:
+    return torch.empty(int(_lib.load().pipnet_train_partials_floats(c)), device=device, dtype=torch.float32)
+
+
+def gelu_fwd(h: Tensor) -> Tensor:
+    _chk(h, "gelu input")
+    g = torch.empty_like(h)
+    _lib.call("pipnet_gelu_fwd_f32", h.data_ptr(), g.data_ptr(), h.numel(), _stream(h))
+    return g
+
+
+def resid_scale(x: Tensor, y2: Tensor, ls: Tensor, row_scale: Optional[Tensor], rows_per_scale: int,
+                out: Optional[Tensor] = None) -> Tensor:
+    """out = x + row_scale[m // rows_per_scale] * (ls * y2) on [M, C] rows."""
+    for t, what in ((x, "residual"), (y2, "branch"), (ls, "layer scale")):
+        _chk(t, what)
+    m, c = x.shape
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("pipnet_resid_scale_f32", x.data_ptr(), y2.data_ptr(), ls.data_ptr(), _ptr(row_scale), rows_per_scale,
+              m, c, out.data_ptr(), _stream(x))
+    return out
+
+
+def ls_backward(dy: Tensor, y2: Tensor, ls: Tensor, row_scale: Optional[Tensor], rows_per_scale: int,
+                d_ls: Tensor, d_b2: Tensor, accumulate: bool = False) -> Tensor:
+    """Backward of resid_scale w.r.t. y2 (returned), ls and the Linear2 bias (into d_ls / d_b2)."""
+    _chk(dy, "dy")
+    _chk(y2, "y2")
+    m, c = dy.shape
+    dy2 = torch.empty_like(dy)
+    _lib.call("pipnet_ls_bwd_f32", dy.data_ptr(), y2.data_ptr(), ls.data_ptr(), _ptr(row_scale), rows_per_scale, m, c,
+              dy2.data_ptr(), d_ls.data_ptr(), d_b2.data_ptr(), int(accumulate), _partials(c, dy.device).data_ptr(),
+              _stream(dy))
+    return dy2
+
+
+def ln_backward(z: Tensor, dt: Tensor, gamma: Tensor, d_gamma: Tensor, d_beta: Tensor, want_dz: bool = True,
+                accumulate: bool = False) -> Optional[Tensor]:
+    """LayerNorm(C, eps 1e-6) backward from the pre-norm rows z [M, C]."""
+    _chk(z, "LN input")
+    _chk(dt, "LN output gradient")
+    m, c = z.shape
+    dz = torch.empty_like(z) if want_dz else None
+    _lib.call("pipnet_ln_bwd_f32", z.data_ptr(), dt.data_ptr(), gamma.data_ptr(), m, c, _ptr(dz), d_gamma.data_ptr(),
+              d_beta.data_ptr(), int(accumulate), _partials(c, z.device).data_ptr(), _stream(z))
+    return dz
+
+
+def dwconv7_plain(x_nhwc: Tensor, w_packed: Tensor, bias: Optional[Tensor], out: Optional[Tensor] = None,
+                  accumulate: bool = False) -> Tensor:
+    """(out +)= [bias] + depthwise 7x7 pad 3 of x (w_packed [49, C])."""
+    _chk(x_nhwc, "dwconv input")
+    b, h, w, c = x_nhwc.shape
+    out = torch.empty_like(x_nhwc) if out is None else out
+    _lib.call("pipnet_dwconv7_plain_f32", x_nhwc.data_ptr(), b, h, w, c, w_packed.data_ptr(), _ptr(bias),
+              int(accumulate), out.data_ptr(), _stream(x_nhwc))
+    return out
+
+
+def dwconv7_wgrad(dz_nhwc: Tensor, x_nhwc: Tensor, dw_packed: Tensor, db: Tensor, accumulate: bool = False) -> None:
+    b, h, w, c = x_nhwc.shape
+    _lib.call("pipnet_dwconv7_wgrad_f32", dz_nhwc.data_ptr(), x_nhwc.data_ptr(), b, h, w, c, dw_packed.data_ptr(),
+              db.data_ptr(), int(accumulate), _partials(c, x_nhwc.device).data_ptr(), _stream(x_nhwc))
+
+
+def wgrad_conv2x2(dy_nhwc: Tensor, x_nhwc: Tensor, stride: int, out: Tensor, accumulate: bool = False) -> Tensor:
+    """Packed [Cout, 4*Cin] weight gradient of the 2x2 downsample conv."""
+    b, h, w, cin = x_nhwc.shape
+    cout = dy_nhwc.shape[-1]
+    nbytes = _lib.load().pipnet_wgrad_workspace_bytes(dy_nhwc.numel() // cout, cout, 4 * cin)
+    ws = torch.empty(max(nbytes // 4, 1), device=x_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_wgrad_conv2x2_f32", dy_nhwc.data_ptr(), x_nhwc.data_ptr(), b, h, w, cin, stride, cout,
+              out.data_ptr(), int(accumulate), ws.data_ptr(), _stream(x_nhwc))
+    return out
+
+
+def head_backward(proto_nhwc: Tensor, pooled: Tensor, d_out: Optional[Tensor], w: Optional[Tensor],
+                  w_align: float, w_tanh: float, tanh_coeff: float = 1.0) -> Tensor:
+    """d loss / d logits of the PIP-Net head (softmax + max-pool) for the align / tanh /
+    classifier terms of calculate_loss (pipnet/train.py:154-265)."""
+    _chk(proto_nhwc, "proto features")
+    n, h, ww, p = proto_nhwc.shape
+    d_logits = torch.empty_like(proto_nhwc)
+    amax = torch.empty((n, p), device=proto_nhwc.device, dtype=torch.int32)
+    dpool = torch.empty((n, p), device=proto_nhwc.device, dtype=torch.float32)
+    k = 0 if w is None else w.shape[0]
+    _lib.call("pipnet_head_bwd_f32", proto_nhwc.data_ptr(), pooled.data_ptr(), n // 2, h * ww, p, _ptr(d_out), _ptr(w),
+              k, w_align, w_tanh, tanh_coeff, amax.data_ptr(), dpool.data_ptr(), d_logits.data_ptr(),
+              _stream(proto_nhwc))
+    return d_logits

@@ -40,6 +40,7 @@ extern "C" {
 #define PIPNET_EPI_BIAS_RESID_RELU 6 /* C = relu(A W^T + b + R) (Bottleneck conv3+BN+identity+ReLU) */
 #define PIPNET_EPI_RESID_ROWSCALE 7  /* C = R + rs[m/g] * (s * (A W^T + b))  (pipnet_linear_rowscale_f32:
                                         CNBlock Linear2 with train-mode stochastic depth)              */
+#define PIPNET_EPI_GELU_BWD 8        /* C = (A W^T) * gelu_erf'(R)   (training: d pre-GELU activation) */
 
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -280,9 +281,49 @@ int pipnet_clamp_min_f32(float* x, int64_t n, float lo, void* stream);
 int64_t pipnet_wgrad_workspace_bytes(int M, int N1, int N2);
 int pipnet_wgrad_f32(const float* A, int64_t lda, const float* B, int64_t ldb, int M, int N1, int N2, float* C,
                      int64_t ldc, int accumulate, float* workspace, void* stream);
+/* pipnet_wgrad_conv2x2_f32: weight gradient of the 2x2 downsample conv (stride 1 or 2):
+ *   dW[co][(ky*2+kx)*Cin + ci] (+)= sum_{b,oy,ox} dY[b,oy,ox,co] x[b, oy*s+ky, ox*s+kx, ci]
+ *   (the packed layout of pipnet_conv2x2_f32's weights); dY NHWC [B,OH,OW,Cout], x NHWC
+ *   [B,H,W,Cin]; workspace: pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, 4*Cin) bytes. */
+int pipnet_wgrad_conv2x2_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int stride, int Cout,
+                             float* dW, int accumulate, float* workspace, void* stream);
 int pipnet_colsum_workspace_bytes(int N);
 int pipnet_colsum_f32(const float* A, int64_t lda, int M, int N, float* out, int accumulate, float* workspace,
                       void* stream);
+
+/* ---- training backward of the trainable ConvNeXt suffix + PIP-Net head ----
+ * Per-channel parameter gradients go through ``partial`` (device scratch of
+ * pipnet_train_partials_floats(C) floats) and a fixed-order reduction; ``accumulate``
+ * adds into the output instead of overwriting.  M = pixels (B*H*W), rows of C channels.
+ * pipnet_gelu_fwd_f32: g = gelu_erf(h) (train forward keeps h for the backward).
+ * pipnet_resid_scale_f32: out = x + row_scale[m / rows_per_scale] * (ls * y2)
+ *   (CNBlock output with layer scale and stochastic depth; row_scale may be NULL).
+ * pipnet_ls_bwd_f32: its backward w.r.t. y2 (dy2 = dy * ls * r), ls and the Linear2 bias.
+ * pipnet_ln_bwd_f32: LayerNorm(C, eps 1e-6) backward from the pre-norm input z:
+ *   dz (NULL to skip), d_gamma, d_beta.
+ * pipnet_dwconv7_plain_f32: y (+)= [bias] + depthwise 7x7 pad 3 of x, w_packed [49][C]
+ *   (the input gradient uses the spatially flipped taps, no bias, accumulate = 1).
+ * pipnet_dwconv7_wgrad_f32: depthwise 7x7 weight ([49][C] packed) and bias gradients.
+ * pipnet_head_bwd_f32: d loss / d logits of the PIP-Net head (softmax over P, max-pool over
+ *   HW) for the align (w_align), tanh (w_tanh) and -- when d_out != NULL -- classifier terms
+ *   (pipnet/train.py:154-265); proto NHWC [2Bh][HW][P], pooled [2Bh][P], W [K][P];
+ *   argmax_ws int32 [2Bh*P], dpool_ws float [2Bh*P]. */
+int64_t pipnet_train_partials_floats(int C);
+int pipnet_gelu_fwd_f32(const float* h, float* g, int64_t n, void* stream);
+int pipnet_resid_scale_f32(const float* x, const float* y2, const float* ls, const float* row_scale,
+                           int rows_per_scale, int64_t M, int C, float* out, void* stream);
+int pipnet_ls_bwd_f32(const float* dy, const float* y2, const float* ls, const float* row_scale, int rows_per_scale,
+                      int64_t M, int C, float* dy2, float* d_ls, float* d_b2, int accumulate, float* partial,
+                      void* stream);
+int pipnet_ln_bwd_f32(const float* z, const float* dt, const float* gamma, int64_t M, int C, float* dz,
+                      float* d_gamma, float* d_beta, int accumulate, float* partial, void* stream);
+int pipnet_dwconv7_plain_f32(const float* x, int B, int H, int W, int C, const float* w_packed, const float* bias,
+                             int accumulate, float* y, void* stream);
+int pipnet_dwconv7_wgrad_f32(const float* dz, const float* x, int B, int H, int W, int C, float* dw_packed,
+                             float* db, int accumulate, float* partial, void* stream);
+int pipnet_head_bwd_f32(const float* proto, const float* pooled, int Bh, int HW, int P, const float* d_out,
+                        const float* W, int K, float w_align, float w_tanh, float tanh_coeff, int32_t* argmax_ws,
+                        float* dpool_ws, float* d_logits, void* stream);
 
 #ifdef __cplusplus
 }
