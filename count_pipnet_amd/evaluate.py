@@ -64,7 +64,7 @@ def eval_pipnet(net, test_loader, epoch, device, log=None, progress_prefix: str 
         xs, ys = xs.to(device, non_blocking=True), ys.to(device, non_blocking=True)
         if enforce_weight_sparsity:
             w = mod._classification.weight
-            K.weight_sparsify_(w.data, THRESHOLD)
+            K.weight_sparsify_(w.detach(), THRESHOLD)
             _bump_version(w)
         _, pooled, out = net(xs, inference=True)
         w_scores = classification_weights if is_count_pipnet else mod._classification.weight

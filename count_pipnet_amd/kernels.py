@@ -410,10 +410,19 @@ def count_encode(x: Tensor, c: int, kind: int, do_round: bool, w: Optional[Tenso
 
 # ---- eval_pipnet metric loop ------------------------------------------------------------
 
+def _mutated(*ts: Tensor) -> None:
+    """A kernel wrote these tensors through raw pointers: bump their in-place version
+    counters, as a torch in-place op would, so version-keyed caches (packed weights) and
+    autograd's saved-tensor checks see the change."""
+    for t in ts:
+        torch.autograd.graph.increment_version(t)
+
+
 def weight_sparsify_(w: Tensor, delta: float = 1e-3) -> Tensor:
     """In place: w = max(w - delta, 0) (pipnet/test.py:73)."""
     _chk(w, "classification weight")
     _lib.call("pipnet_weight_sparsify_f32", w.data_ptr(), w.numel(), delta, _stream(w))
+    _mutated(w)
     return w
 
 
@@ -544,11 +553,13 @@ def adamw_step_(param: Tensor, grad: Tensor, exp_avg: Tensor, exp_avg_sq: Tensor
     _lib.call("pipnet_adamw_step_f32", param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(),
               exp_avg_sq.data_ptr(), param.numel(), lr, beta1, beta2, eps, weight_decay, int(step),
               int(post is not None), delta, floor, _stream(param))
+    _mutated(param, exp_avg, exp_avg_sq)
 
 
 def clamp_min_(x: Tensor, lo: float) -> Tensor:
     _chk(x, "tensor")
     _lib.call("pipnet_clamp_min_f32", x.data_ptr(), x.numel(), lo, _stream(x))
+    _mutated(x)
     return x
 
 

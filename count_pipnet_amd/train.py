@@ -114,7 +114,7 @@ def hip_adamw_step(optimizer: torch.optim.Optimizer, param: Tensor, grad: Tensor
         st["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
     st["step"] += 1
     beta1, beta2 = g["betas"]
-    K.adamw_step_(param.data, grad, st["exp_avg"], st["exp_avg_sq"], float(g["lr"]), beta1, beta2,
+    K.adamw_step_(param.detach(), grad, st["exp_avg"], st["exp_avg_sq"], float(g["lr"]), beta1, beta2,
                   float(g["eps"]), float(g["weight_decay"]), int(st["step"].item()), post)
     return True
 
@@ -148,49 +148,273 @@ def hip_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor,
             stepped_b = hip_adamw_step(optimizer_classifier, cls.bias, db, clamp_b)
         if enforce_weight_sparsity:          # the clamps of parameters the optimizer did not touch
             if not stepped_w:
-                K.weight_sparsify_(cls.weight.data, SPARSITY_DELTA)
+                K.weight_sparsify_(cls.weight.detach(), SPARSITY_DELTA)
             if cls.bias is not None and not stepped_b:
-                K.clamp_min_(cls.bias.data, 0.0)
-            K.clamp_min_(cls.normalization_multiplier.data, 1.0)
+                K.clamp_min_(cls.bias.detach(), 0.0)
+            K.clamp_min_(cls.normalization_multiplier.detach(), 1.0)
     return stats
 
 
-class FinetuneEpoch:
-    """Runs finetune iterations back to back with all bookkeeping on the device.
+# ------------------------------------------------------------------------------------------
+# Pretrain / joint phases: a trainable backbone suffix + add-on (+ classifier) on the HIP
+# kernels (main.py:238-256 pretrain, :377-390 "train + freeze params")
+# ------------------------------------------------------------------------------------------
+def _cnblocks(seq) -> list:
+    return [b for mod in seq if isinstance(mod, nn.Sequential) for b in mod if isinstance(b, CNBlock)]
 
-    Per batch (view-1 images, view-2 images, labels): ``hip_finetune_step``, then the
-    classifier LR schedule is advanced to the fractional epoch position of the next batch
-    (CosineAnnealingWarmRestarts is stepped with a float epoch in the reference,
-    train.py:120).  The five running sums (align, tanh, class, loss, accuracy) live in one
-    device vector; ``summary()`` is the single host read."""
+
+def trainable_suffix_start(net: nn.Module) -> int:
+    """Index j of the first ``features`` entry holding a trainable parameter (len(features)
+    when the backbone is frozen).  Gradients flow through every entry of features[j:]."""
+    for j, mod in enumerate(_inner(net)._net.features):
+        if any(p.requires_grad for p in mod.parameters()):
+            return j
+    return len(_inner(net)._net.features)
+
+
+def hip_train_supported(net: nn.Module) -> bool:
+    """A ConvNeXt PIP-Net (fp32, ROCm) whose trainable backbone part is a suffix that does
+    not include the stem (the reference's pretrain / frozen phases)."""
+    m = _inner(net)
+    if hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+        return False
+    if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
+        return False
+    return trainable_suffix_start(m) >= 1
+
+
+def _forward_saving(m: nn.Module, xs: Tensor, j: int, sd_keep: Dict[int, Tensor]):
+    """Train-mode forward; features[:j] on the inference executor, features[j:] with plain
+    (unfused) kernels whose intermediates are kept: per CNBlock the input x, the depthwise
+    output z, the LayerNorm output t, the Linear1 pre-activation h1, GELU output g and the
+    Linear2 output y2; per downsample its input and LayerNorm output."""
+    from . import _lib
+    from .convnext_features import LayerNorm2d, packed, stochastic_depth_row_scales
+    feats, cache = m._net.features, m._net._hip_pack
+    h = convnext_features_hip(feats[:j], xs, cache, sd_keep)
+    scales = stochastic_depth_row_scales(feats, sd_keep, xs.shape[0], xs.device)
+    saved = []
+    bid = len(_cnblocks(feats[:j]))
+    for idx in range(j, len(feats)):
+        mod = feats[idx]
+        if len(mod) > 0 and isinstance(mod[0], CNBlock):
+            for jb, blk in enumerate(mod):
+                dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
+                b, hh, ww, c = h.shape
+                key = f"{idx}.{jb}"
+                wdw = packed(cache, key + ".dw", dw.weight, lambda w: w.reshape(c, 49).t())
+                z = K.dwconv7_plain(h, wdw, dw.bias)
+                t = K.layernorm(z, ln.weight, ln.bias)
+                h1 = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS)
+                g = K.gelu_fwd(h1)
+                y2 = K.linear(g, l2.weight, l2.bias, _lib.EPI_BIAS)
+                rs = scales.get(bid) if blk.stochastic_depth.p > 0.0 else None
+                out = K.resid_scale(h.view(-1, c), y2, blk.layer_scale.view(-1), rs, hh * ww).view(b, hh, ww, c)
+                saved.append(("block", blk, key, dict(x=h, z=z, t=t, h1=h1, g=g, y2=y2, rs=rs)))
+                h = out
+                bid += 1
+        elif len(mod) == 2 and isinstance(mod[0], LayerNorm2d) and isinstance(mod[1], nn.Conv2d):
+            ln, conv = mod[0], mod[1]
+            t = K.layernorm(h, ln.weight, ln.bias)
+            wp = packed(cache, f"{idx}.conv", conv.weight, lambda w: w.permute(0, 2, 3, 1))
+            out = K.conv2x2(t, wp, conv.bias, conv.stride[0])
+            saved.append(("down", mod, f"{idx}.conv", dict(x=h, t=t)))
+            h = out
+        else:
+            raise RuntimeError(f"HIP training step: unsupported ConvNeXt features entry {idx}")
+    return h, saved
+
+
+def _set_grad(p: Tensor, g: Tensor) -> None:
+    if p.requires_grad:
+        p.grad = g.reshape(p.shape).contiguous()
+
+
+def _block_backward(blk: CNBlock, sv: dict, dy: Tensor) -> Tensor:
+    """Gradients of one CNBlock (written to the parameters' .grad); returns d input [B,H,W,C]."""
+    from . import _lib
+    dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
+    x = sv["x"]
+    b, hh, ww, c = x.shape
+    dev = x.device
+    d_ls, d_b2 = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    dyv = dy.reshape(-1, c)
+    dy2 = K.ls_backward(dyv, sv["y2"], blk.layer_scale.view(-1), sv["rs"], hh * ww, d_ls, d_b2)
+    _set_grad(blk.layer_scale, d_ls)
+    _set_grad(l2.bias, d_b2)
+    if l2.weight.requires_grad:
+        _set_grad(l2.weight, K.wgrad(dy2, sv["g"]))
+    dh1 = K.linear(dy2, l2.weight.t().contiguous(), None, _lib.EPI_GELU_BWD, r=sv["h1"])
+    if l1.weight.requires_grad:
+        _set_grad(l1.weight, K.wgrad(dh1, sv["t"].view(-1, c)))
+    if l1.bias.requires_grad:
+        _set_grad(l1.bias, K.colsum(dh1))
+    dt = K.linear(dh1, l1.weight.t().contiguous(), None, _lib.EPI_NONE)
+    d_lnw, d_lnb = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    dz = K.ln_backward(sv["z"].view(-1, c), dt, ln.weight, d_lnw, d_lnb, want_dz=True).view(b, hh, ww, c)
+    _set_grad(ln.weight, d_lnw)
+    _set_grad(ln.bias, d_lnb)
+    dwp, d_dwb = torch.empty(49, c, device=dev), torch.empty(c, device=dev)
+    K.dwconv7_wgrad(dz, x, dwp, d_dwb)
+    _set_grad(dw.weight, dwp.t())
+    _set_grad(dw.bias, d_dwb)
+    wflip = dw.weight.detach().flip(2, 3).reshape(c, 49).t().contiguous()
+    dx = dy.reshape(b, hh, ww, c)                    # residual path; the branch's input grad adds in place
+    K.dwconv7_plain(dz, wflip, None, out=dx, accumulate=True)
+    return dx
+
+
+def _down_backward(mod: nn.Sequential, sv: dict, dy: Tensor, need_dx: bool) -> Optional[Tensor]:
+    """LayerNorm2d + Conv2d(k2, stride 1|2) backward; returns d input when ``need_dx``."""
+    from . import _lib
+    ln, conv = mod[0], mod[1]
+    x, t = sv["x"], sv["t"]
+    b, h, w, cin = t.shape
+    cout, stride = conv.out_channels, conv.stride[0]
+    if conv.weight.requires_grad:
+        gp = torch.empty(cout, 4 * cin, device=t.device)
+        K.wgrad_conv2x2(dy, t, stride, gp)
+        _set_grad(conv.weight, gp.view(cout, 2, 2, cin).permute(0, 3, 1, 2))
+    if conv.bias is not None and conv.bias.requires_grad:
+        _set_grad(conv.bias, K.colsum(dy.reshape(-1, cout)))
+    if not (ln.weight.requires_grad or ln.bias.requires_grad or need_dx):
+        return None
+    wd = conv.weight.detach()
+    if stride == 1:        # transposed conv = conv of dy (pad 1) with the flipped, transposed taps
+        dt = K.conv2d_nhwc(dy.contiguous(), wd.permute(1, 2, 3, 0).flip(1, 2).contiguous(), None, 1, 1,
+                           _lib.EPI_NONE)
+    else:                  # stride 2: taps do not overlap -> one GEMM, then place the 2x2 blocks
+        oh, ow = dy.shape[1], dy.shape[2]
+        gm = K.linear(dy.reshape(-1, cout), wd.permute(2, 3, 1, 0).reshape(4 * cin, cout).contiguous(), None,
+                      _lib.EPI_NONE)
+        dt = torch.zeros(b, h, w, cin, device=t.device)
+        dt[:, :2 * oh, :2 * ow] = gm.view(b, oh, ow, 2, 2, cin).permute(0, 1, 3, 2, 4, 5).reshape(b, 2 * oh, 2 * ow, cin)
+    d_lnw, d_lnb = torch.empty(cin, device=t.device), torch.empty(cin, device=t.device)
+    dx = K.ln_backward(x.reshape(-1, cin), dt.reshape(-1, cin), ln.weight, d_lnw, d_lnb, want_dz=need_dx)
+    _set_grad(ln.weight, d_lnw)
+    _set_grad(ln.bias, d_lnb)
+    return None if dx is None else dx.view(b, h, w, cin)
+
+
+def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimizer_net, optimizer_classifier,
+                   pretrain: bool, epoch: int, nr_epochs: int, enforce_weight_sparsity: bool = True,
+                   sd_keep: Optional[Dict[int, Tensor]] = None, generator: Optional[torch.Generator] = None,
+                   step_optimizers: bool = True) -> Tensor:
+    """One pretrain (``pretrain=True``) or joint iteration (train.py:75-140 with
+    finetune=False) for a trainable backbone suffix: train-mode forward keeping the
+    suffix's activations, the loss kernel, backward through head, add-on and suffix (every
+    parameter with requires_grad gets its .grad), then optimizer_classifier (joint only)
+    and optimizer_net steps (AdamW on the device) and the sparsity clamps.  Returns the
+    loss-kernel stats without synchronising."""
+    from . import _lib
+    from .pipnet import add_on_logits_hip
+    m = _inner(net)
+    j = trainable_suffix_start(m)
+    if j < 1:
+        raise NotImplementedError("HIP training step: the ConvNeXt stem is trainable (not supported)")
+    xs = torch.cat([xs1, xs2])
+    if sd_keep is None:
+        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+    cls = m._classification
+    w_align, w_tanh, w_class = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
+    with torch.no_grad():
+        feats, saved = _forward_saving(m, xs, j, sd_keep)
+        logits = add_on_logits_hip(m._add_on, feats)
+        proto, pooled = K.softmax_pool(logits, pool_mode=0)
+        _, out = K.nonneg_linear(pooled, cls.weight, cls.bias, None)
+        stats, d_out = K.train_loss(proto, pooled, out, ys, cls.normalization_multiplier, enforce_weight_sparsity,
+                                    1.0, w_align, w_tanh, w_class, "pretrain" if pretrain else "train")
+        if d_out is not None and (cls.weight.requires_grad or (cls.bias is not None and cls.bias.requires_grad)):
+            dw, db = K.nonneg_linear_backward(d_out, pooled, cls.weight, cls.bias is not None)
+            _set_grad(cls.weight, dw)
+            if cls.bias is not None:
+                _set_grad(cls.bias, db)
+        d_logits = K.head_backward(proto, pooled, d_out, cls.weight, w_align, w_tanh)
+        mods = list(m._add_on) if isinstance(m._add_on, nn.Sequential) else [m._add_on]
+        if len(mods) == 2:                           # 1x1 prototype conv before the softmax
+            conv = mods[0]
+            bsz, hh, ww, cf = feats.shape
+            pn = conv.out_channels
+            dl = d_logits.view(-1, pn)
+            if conv.weight.requires_grad:
+                _set_grad(conv.weight, K.wgrad(dl, feats.view(-1, cf)))
+            if conv.bias is not None and conv.bias.requires_grad:
+                _set_grad(conv.bias, K.colsum(dl))
+            dy = K.linear(dl, conv.weight.detach().view(pn, cf).t().contiguous(), None, _lib.EPI_NONE)
+            dy = dy.view(bsz, hh, ww, cf)
+        else:
+            dy = d_logits
+        for i in range(len(saved) - 1, -1, -1):
+            kind, mod, _, sv = saved[i]
+            if kind == "block":
+                dy = _block_backward(mod, sv, dy)
+            else:
+                dy = _down_backward(mod, sv, dy, need_dx=i > 0)
+            saved[i] = None                          # free the activations as we go
+        if step_optimizers:
+            if not pretrain:
+                for g in optimizer_classifier.param_groups:
+                    for p in g["params"]:
+                        if p.grad is not None:
+                            post = None
+                            if enforce_weight_sparsity:
+                                post = (SPARSITY_DELTA, 0.0) if p is cls.weight else (0.0, 0.0) if p is cls.bias else None
+                            hip_adamw_step(optimizer_classifier, p, p.grad, post)
+            for g in optimizer_net.param_groups:
+                for p in g["params"]:
+                    if p.grad is not None:
+                        hip_adamw_step(optimizer_net, p, p.grad)
+            if not pretrain and enforce_weight_sparsity:
+                if not cls.weight.requires_grad:
+                    K.weight_sparsify_(cls.weight.detach(), SPARSITY_DELTA)
+                if cls.bias is not None and not cls.bias.requires_grad:
+                    K.clamp_min_(cls.bias.detach(), 0.0)
+                K.clamp_min_(cls.normalization_multiplier.detach(), 1.0)
+    return stats
+
+
+# ------------------------------------------------------------------------------------------
+# epoch loop (train.py:8-150 drop-in)
+# ------------------------------------------------------------------------------------------
+class HipEpoch:
+    """Runs HIP training iterations back to back with all bookkeeping on the device.
+
+    Per batch (view-1 images, view-2 images, labels): one device step, then the schedules
+    advance as in the reference -- the classifier's CosineAnnealingWarmRestarts to the
+    fractional epoch position (train.py:120, not in pretrain), the backbone's scheduler once
+    per iteration (train.py:124-126, not in finetune).  The five running sums (align, tanh,
+    class, loss, accuracy) live in one device vector; ``summary()`` is the single host read."""
 
     TERMS = ("align", "tanh", "class")
 
-    def __init__(self, net: nn.Module, optimizer: torch.optim.Optimizer, enforce_weight_sparsity: bool = True,
-                 generator: Optional[torch.Generator] = None):
-        self.net, self.optimizer = net, optimizer
-        self.enforce = enforce_weight_sparsity
-        self.generator = generator
+    def __init__(self, step, weights: Tuple[float, float, float], track_acc: bool):
+        self.step, self.weights, self.track_acc = step, weights, track_acc
         self.sums: Optional[Tensor] = None
         self.count = 0
-        self.lrs: list = []
+        self.lrs_class: list = []
+        self.lrs_net: list = []
 
-    def add(self, stats: Tensor, labels: int) -> None:
-        acc = stats[4:5] / float(2 * labels)
+    def _add(self, stats: Tensor, labels: int) -> None:
+        acc = stats[4:5] / float(2 * labels) if self.track_acc else torch.zeros_like(stats[4:5])
         row = torch.cat([stats[:4], acc]).double()
         self.sums = row if self.sums is None else self.sums.add_(row)
         self.count += 1
 
-    def run(self, batches, scheduler, epoch: int, device, extra_optimizers=()) -> None:
+    def run(self, batches, optimizers, epoch: int, device, scheduler_classifier=None, scheduler_net=None) -> None:
         n_batches = len(batches)
         for pos, batch in enumerate(batches):
             a, b, labels = (t.to(device, non_blocking=True) for t in batch)
-            for opt in (self.optimizer, *extra_optimizers):
+            for opt in optimizers:
                 opt.zero_grad(set_to_none=True)
-            self.add(hip_finetune_step(self.net, a, b, labels, self.optimizer, self.enforce,
-                                       generator=self.generator), labels.shape[0])
-            scheduler.step((epoch - 1) + pos / n_batches)
-            self.lrs.append(scheduler.get_last_lr()[0])
+            self._add(self.step(a, b, labels), labels.shape[0])
+            if scheduler_classifier is not None:
+                scheduler_classifier.step((epoch - 1) + pos / n_batches)
+                self.lrs_class.append(scheduler_classifier.get_last_lr()[0])
+            if scheduler_net is not None:
+                scheduler_net.step()
+                self.lrs_net.append(scheduler_net.get_last_lr()[0])
+            else:
+                self.lrs_net.append(0.0)
 
     def summary(self) -> dict:
         vals = self.sums.cpu().tolist() if self.sums is not None else [0.0] * 5
@@ -198,9 +422,9 @@ class FinetuneEpoch:
         info = {}
         for j, term in enumerate(self.TERMS):
             info[f"{term}_loss_raw"] = vals[j] / n
-            info[f"{term}_loss_weighted"] = vals[j] / n * FINETUNE_LOSS_WEIGHTS[j]
-        info.update(train_accuracy=vals[4] / n, loss=vals[3] / n, lrs_net=[0.0] * self.count,
-                    lrs_class=list(self.lrs))
+            info[f"{term}_loss_weighted"] = vals[j] / n * self.weights[j]
+        info.update(train_accuracy=vals[4] / n, loss=vals[3] / n, lrs_net=list(self.lrs_net),
+                    lrs_class=list(self.lrs_class))
         return info
 
 
@@ -208,20 +432,38 @@ def train_pipnet(net, train_loader, optimizer_net, optimizer_classifier, schedul
                  criterion, epoch, nr_epochs, device, is_count_pipnet=False, pretrain=False, finetune=False,
                  progress_prefix: str = "Train Epoch", enforce_weight_sparsity=True, tanh_loss_coeff=1.0,
                  generator: Optional[torch.Generator] = None, verbose: bool = False) -> dict:
-    """Drop-in for train.py:8-150 in the finetune phase (same arguments, same ``train_info``
-    keys; progress output reduced to one optional line).  Other phases raise: run the
-    reference's own loop on this package's modules (torch autograd path)."""
-    if pretrain or not finetune or is_count_pipnet or not hip_finetune_supported(net):
+    """Drop-in for train.py:8-150 (same arguments, same ``train_info`` keys; progress output
+    reduced to one optional line) for a ConvNeXt PIP-Net: the finetune phase
+    (``hip_finetune_step``) and the pretrain / joint phases with a trainable backbone suffix
+    (``hip_train_step``).  Anything else (CountPIPNet, ResNet, a trainable stem) raises --
+    run the reference's own loop on these modules (torch autograd path)."""
+    if is_count_pipnet or (pretrain and finetune):
+        raise NotImplementedError("count_pipnet_amd.train_pipnet: CountPIPNet training runs on the torch path")
+    if finetune and hip_finetune_supported(net):
+        weights = FINETUNE_LOSS_WEIGHTS
+
+        def step(a, b, labels):
+            return hip_finetune_step(net, a, b, labels, optimizer_classifier, enforce_weight_sparsity,
+                                     generator=generator)
+    elif not finetune and hip_train_supported(net):
+        weights = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
+
+        def step(a, b, labels):
+            return hip_train_step(net, a, b, labels, optimizer_net, optimizer_classifier, pretrain, epoch,
+                                  nr_epochs, enforce_weight_sparsity, generator=generator)
+    else:
         raise NotImplementedError(
-            "count_pipnet_amd.train_pipnet runs the finetune phase of a ConvNeXt PIP-Net on the HIP kernels; "
-            "for other phases use the reference train_pipnet with these modules (torch autograd path)")
+            "count_pipnet_amd.train_pipnet: this configuration (phase / trainable parameters / device) has no HIP "
+            "step; use the reference train_pipnet with these modules (torch autograd path)")
     net.train()
-    _inner(net)._classification.requires_grad = True
-    runner = FinetuneEpoch(net, optimizer_classifier, enforce_weight_sparsity, generator)
-    extra = (optimizer_net,) if optimizer_net is not None and optimizer_net is not optimizer_classifier else ()
-    runner.run(train_loader, scheduler_classifier, epoch, device, extra)
+    _inner(net)._classification.requires_grad = not pretrain
+    runner = HipEpoch(step, weights, track_acc=not pretrain)
+    opts = [o for o in (optimizer_classifier, optimizer_net) if o is not None]
+    opts = [o for i, o in enumerate(opts) if all(o is not q for q in opts[:i])]
+    runner.run(train_loader, opts, epoch, device, None if pretrain else scheduler_classifier,
+               None if finetune else scheduler_net)
     info = runner.summary()
     if verbose:
-        terms = ", ".join(f"{t}={info[t + '_loss_raw']:.4f}" for t in FinetuneEpoch.TERMS)
-        print(f"[{progress_prefix} {epoch}] finetune on HIP: {runner.count} iterations, {terms}", flush=True)
+        terms = ", ".join(f"{t}={info[t + '_loss_raw']:.4f}" for t in HipEpoch.TERMS)
+        print(f"[{progress_prefix} {epoch}] HIP: {runner.count} iterations, {terms}", flush=True)
     return info

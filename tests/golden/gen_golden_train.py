@@ -44,10 +44,15 @@ sys.path.insert(0, os.path.dirname(HERE))
 from golden_util import train_loader_batches  # noqa: E402
 from count_pipnet_amd.synthetic import synth_bernoulli  # noqa: E402
 
-# name -> (forward golden case, iterations, batch per view, seed, record proto map)
+# name -> (forward golden case, iterations, batch per view, seed, record proto map, phase)
+# phase: "finetune" (main.py:333-345), "joint" (the "train + freeze params" epochs,
+# main.py:377-390) or "pretrain" (main.py:238-256)
 TRAIN_CASES = {
-    "train_finetune_mid_addon": ("pipnet_mid_addon", 3, 3, 301, True),
-    "train_finetune_c2": ("c2_pipnet_convnext26", 2, 2, 302, False),
+    "train_finetune_mid_addon": ("pipnet_mid_addon", 3, 3, 301, True, "finetune"),
+    "train_finetune_c2": ("c2_pipnet_convnext26", 2, 2, 302, False, "finetune"),
+    "train_joint_mid_addon": ("pipnet_mid_addon", 3, 3, 303, True, "joint"),
+    "train_pretrain_mid_addon": ("pipnet_mid_addon", 2, 3, 304, True, "pretrain"),
+    "train_joint_c2": ("c2_pipnet_convnext26", 2, 2, 305, False, "joint"),
 }
 LR, WD = 0.05, 0.01
 
@@ -72,7 +77,7 @@ def injected_bernoulli(seed: int):
 
 
 def run(name):
-    fwd_case, nb, bs, seed, keep_proto = TRAIN_CASES[name]
+    fwd_case, nb, bs, seed, keep_proto, phase = TRAIN_CASES[name]
     net, case = G.build_reference(fwd_case)
     sys.path.insert(0, G.REF)
     import pipnet.train as ref_train
@@ -82,11 +87,15 @@ def run(name):
                               num_stages=case.get("num_stages", 2), bias=case["bias"], lr=LR, lr_net=5e-4,
                               lr_block=5e-4, weight_decay=WD, optimizer="Adam", seed=1, train_intermediate=False)
     with contextlib.redirect_stdout(io.StringIO()):
-        opt_net, opt_cls, _, _, _ = get_optimizer_nn(dp, args)
+        opt_net, opt_cls, to_freeze, to_train, backbone = get_optimizer_nn(dp, args)
     for p in net.parameters():                       # main.py:335-339 (finetune)
         p.requires_grad = False
     for p in net._classification.parameters():
-        p.requires_grad = True
+        p.requires_grad = phase != "pretrain"
+    if phase != "finetune":                          # main.py:240-249 / 377-385
+        for group in (to_train, to_freeze, list(net._add_on.parameters())):
+            for p in group:
+                p.requires_grad = True
     net._classification.normalization_multiplier.requires_grad = False
     sched_net = torch.optim.lr_scheduler.CosineAnnealingLR(opt_net, T_max=10, eta_min=5e-6)
     sched_cls = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt_cls, T_0=10, eta_min=0.001, T_mult=1)
@@ -115,9 +124,11 @@ def run(name):
     try:
         with injected_bernoulli(seed=5000 + seed) as drawn, contextlib.redirect_stdout(io.StringIO()), \
                 contextlib.redirect_stderr(io.StringIO()):
-            info = ref_train.train_pipnet(dp, batches, opt_net, opt_cls, sched_net, sched_cls, criterion, 1, 1,
-                                          torch.device("cpu"), is_count_pipnet=False, pretrain=False,
-                                          finetune=True, enforce_weight_sparsity=True)
+            info = ref_train.train_pipnet(dp, batches, opt_net, opt_cls,
+                                          sched_net, None if phase == "pretrain" else sched_cls, criterion,
+                                          1, 2 if phase == "pretrain" else 1, torch.device("cpu"),
+                                          is_count_pipnet=False, pretrain=phase == "pretrain",
+                                          finetune=phase == "finetune", enforce_weight_sparsity=True)
     finally:
         h.remove()
         ref_train.calculate_loss = orig_loss
@@ -140,17 +151,29 @@ def run(name):
                 rec[f"s{i}_{k}"] = s[k].numpy()
         if keep_proto:
             rec[f"s{i}_w"] = s["w"].numpy()
+    if phase != "finetune":      # every trainable backbone / add-on tensor: full when small, else checksums
+        for pname, prm in net.named_parameters():
+            if prm.requires_grad and not pname.startswith("_classification"):
+                a = prm.detach().double()
+                rec[f"param/{pname}/sum"] = np.array(float(a.sum()))
+                rec[f"param/{pname}/abs"] = np.array(float(a.abs().sum()))
+                rec[f"param/{pname}/head"] = prm.detach().flatten()[:256].numpy()
+                st_p = opt_net.state.get(prm, {})
+                if "exp_avg_sq" in st_p:
+                    rec[f"param/{pname}/v_head"] = st_p["exp_avg_sq"].flatten()[:256].numpy()
     cls = net._classification
     put("final_w", cls.weight)
     rec["final_mult"] = cls.normalization_multiplier.detach().numpy()
-    st = opt_cls.state[cls.weight]
+    st = opt_cls.state.get(cls.weight, {"exp_avg": torch.zeros_like(cls.weight),
+                                         "exp_avg_sq": torch.zeros_like(cls.weight), "step": 0.0})
     put("final_w_exp_avg", st["exp_avg"])
     put("final_w_exp_avg_sq", st["exp_avg_sq"])
-    if cls.bias is not None:
+    if cls.bias is not None and cls.bias in opt_cls.state:
         rec["final_b"] = cls.bias.detach().numpy()
         rec["final_b_exp_avg"] = opt_cls.state[cls.bias]["exp_avg"].numpy()
         rec["final_b_exp_avg_sq"] = opt_cls.state[cls.bias]["exp_avg_sq"].numpy()
-    meta = dict(name=name, forward_case=fwd_case, iterations=nb, batch_per_view=bs, seed=seed,
+    meta = dict(name=name, forward_case=fwd_case, phase=phase, iterations=nb, batch_per_view=bs, seed=seed,
+                lr_net=5e-4, lr_block=5e-4,
                 mask_seed=5000 + seed, masks_per_step=nmask, lr=LR, weight_decay=WD,
                 steps=float(st["step"]), components=comps,
                 info={k: (v if isinstance(v, list) else float(v)) for k, v in info.items()},

@@ -25,7 +25,8 @@ from model_util import build_model
 from oracle import ref_cpu, train_ref
 
 pytestmark = pytest.mark.gpu
-NAMES = train_golden_names()
+NAMES = [n for n in train_golden_names() if n.startswith("train_finetune_")]
+SUFFIX = [n for n in train_golden_names() if not n.startswith("train_finetune_")]
 
 
 def _t(a):
@@ -238,3 +239,141 @@ def test_train_forward_stochastic_depth_matches_oracle(gpu):
     torch.testing.assert_close(pooled.cpu(), rpool, rtol=1e-3, atol=2e-4)
     torch.testing.assert_close(out.cpu(), rout, rtol=1e-3, atol=2e-3)
     torch.testing.assert_close(proto.cpu().permute(0, 3, 1, 2), rp, rtol=1e-3, atol=2e-4)
+
+
+# ---- pretrain / joint phases: trainable backbone suffix + add-on (+ classifier) ------------
+def _optimizers_like_reference(net, meta, fwd_meta):
+    """AdamW groups of util/args.py:get_optimizer_nn (restated for the test) + the phase's
+    requires_grad pattern (main.py:238-256 pretrain, 377-390 joint) + its schedulers."""
+    case = fwd_meta["case"]
+    train, freeze, backbone = [], [], []
+    for name, prm in net._net.named_parameters():
+        parts = name.split(".")
+        if case.get("use_mid_layers"):
+            st = int(parts[1])
+            (train if st == case["num_stages"] else freeze if st == case["num_stages"] - 1 else backbone).append(prm)
+        else:
+            (train if "features.7.2" in name else freeze if ("features.7" in name or "features.6" in name)
+             else backbone).append(prm)
+    lr_net, lr_block = meta["lr_net"], meta["lr_block"]
+    opt_net = torch.optim.AdamW([{"params": backbone, "lr": lr_net, "weight_decay": 0.0},
+                                 {"params": freeze, "lr": lr_block, "weight_decay": 0.0},
+                                 {"params": train, "lr": lr_block, "weight_decay": 0.0},
+                                 {"params": list(net._add_on.parameters()), "lr": lr_block * 10.0, "weight_decay": 0.0}],
+                                lr=meta["lr"], weight_decay=0.0)
+    cls = net._classification
+    groups = [{"params": [cls.weight], "lr": meta["lr"], "weight_decay": meta["weight_decay"]}]
+    if cls.bias is not None:
+        groups.append({"params": [cls.bias], "lr": meta["lr"], "weight_decay": 0.0})
+    opt_cls = torch.optim.AdamW(groups, lr=meta["lr"], weight_decay=0.0)
+    for prm in net.parameters():
+        prm.requires_grad = False
+    for prm in train + freeze + list(net._add_on.parameters()):
+        prm.requires_grad = True
+    for prm in cls.parameters():
+        prm.requires_grad = meta["phase"] != "pretrain"
+    cls.normalization_multiplier.requires_grad = False
+    sched_net = torch.optim.lr_scheduler.CosineAnnealingLR(opt_net, T_max=10, eta_min=5e-6)
+    sched_cls = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt_cls, T_0=10, eta_min=0.001, T_mult=1)
+    return opt_net, opt_cls, sched_net, sched_cls
+
+
+@pytest.mark.parametrize("name", SUFFIX)
+def test_suffix_training_matches_reference(gpu, name):
+    meta, rec, fwd_meta = load_train_golden(name)
+    net = build_model(fwd_meta).to(gpu).train()
+    opt_net, opt_cls, sched_net, sched_cls = _optimizers_like_reference(net, meta, fwd_meta)
+    assert T.hip_train_supported(net)
+    pretrain = meta["phase"] == "pretrain"
+    c = fwd_meta["case"]
+    batches = train_loader_batches(c["size"], c["num_classes"], meta["iterations"], meta["batch_per_view"],
+                                   meta["seed"])
+    iters = len(batches)
+    for i, (xs1, xs2, ys) in enumerate(batches):
+        sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
+        opt_net.zero_grad(set_to_none=True)
+        opt_cls.zero_grad(set_to_none=True)
+        stats = T.hip_train_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt_net, opt_cls, pretrain, 1,
+                                 2 if pretrain else 1, True, sd_keep=sd_keep).cpu()
+        comp = meta["components"][i]
+        assert float(stats[0]) == pytest.approx(comp["align"], rel=2e-3, abs=1e-4)
+        assert float(stats[1]) == pytest.approx(comp["tanh"], rel=2e-3, abs=1e-4)
+        assert float(stats[3]) == pytest.approx(comp["loss"], rel=2e-3, abs=1e-4)
+        if not pretrain:
+            assert float(stats[2]) == pytest.approx(comp["class"], rel=2e-3, abs=1e-4)
+            sched_cls.step(0 + i / iters)
+        sched_net.step()
+    # every trainable backbone / add-on tensor: sums, and the first 256 values elementwise
+    # (99 % quorum: AdamW's first steps move each weight by ~lr * sign(grad))
+    names = [k.split("/")[1] for k in rec if k.startswith("param/") and k.endswith("/sum")]
+    assert names
+    params = dict(net.named_parameters())
+    lr_max = max(g["lr"] for g in opt_net.param_groups) * 1.0
+    for pname in names:
+        p = params[pname].detach().cpu().double()
+        head = _t(rec[f"param/{pname}/head"]).double()
+        _quorum_close(p.flatten()[:head.numel()], head, 1e-4, 1e-6, frac=0.95,
+                      max_abs=2.5 * meta["iterations"] * 10 * meta["lr_block"] + 1e-6)
+        ref_abs = float(rec[f"param/{pname}/abs"])
+        assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
+    cls = net._classification
+    if not pretrain:
+        if "final_w" in rec:
+            _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, frac=0.97,
+                          max_abs=4 * meta["lr"] * iters + 1e-6)
+        else:
+            _quorum_close(cls.weight[:8], _t(rec["final_w_rows8"]), 1e-4, 1e-5, frac=0.97,
+                          max_abs=4 * meta["lr"] * iters + 1e-6)
+
+
+def _torch_path_grads(net, xs, ys, masks_in_order, w_align, w_tanh, w_class, mult):
+    """Autograd reference on the module's torch path (train mode), stochastic-depth masks
+    injected in forward order, loss as calculate_loss (align with detached targets)."""
+    from count_pipnet_amd.backend import torch_backend
+    orig = torch.Tensor.bernoulli_
+    it = iter(masks_in_order)
+
+    def fake(self, p=0.5, *, generator=None):
+        with torch.no_grad():
+            self.copy_(next(it).view(self.shape).to(self.dtype))
+        return self
+
+    torch.Tensor.bernoulli_ = fake
+    try:
+        with torch_backend():
+            proto, pooled, out = net(xs)
+    finally:
+        torch.Tensor.bernoulli_ = orig
+    bh = xs.shape[0] // 2
+    terms = train_ref.loss_terms(proto, pooled, out, ys.cpu().to(out.device), mult)
+    e1, e2 = train_ref.proto_pixels(proto[:bh]), train_ref.proto_pixels(proto[bh:])
+    align = (train_ref.align_loss(e1, e2.detach()) + train_ref.align_loss(e2, e1.detach())) / 2
+    loss = w_align * align + w_tanh * terms["tanh"] + w_class * terms["cls"]
+    loss.backward()
+    return {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("name", SUFFIX)
+def test_suffix_gradients_match_autograd(gpu, name):
+    meta, rec, fwd_meta = load_train_golden(name)
+    net = build_model(fwd_meta).to(gpu).train()
+    opt_net, opt_cls, _, _ = _optimizers_like_reference(net, meta, fwd_meta)
+    pretrain = meta["phase"] == "pretrain"
+    c = fwd_meta["case"]
+    xs1, xs2, ys = train_loader_batches(c["size"], c["num_classes"], 1, meta["batch_per_view"], meta["seed"])[0]
+    sd_keep = _sd_keep(net, rec["s0_masks"])
+    T.hip_train_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt_net, opt_cls, pretrain, 1, 2 if pretrain else 1,
+                     True, sd_keep=sd_keep, step_optimizers=False)
+    hip = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+    for p in net.parameters():
+        p.grad = None
+    wa, wt, wc = (0.5, 5.0, 0.0) if pretrain else (5.0, 2.0, 2.0)
+    masks = [_t(m).float().to(gpu) for m in rec["s0_masks"]]
+    ref = _torch_path_grads(net, torch.cat([xs1, xs2]).to(gpu), ys.to(gpu), masks, wa, wt, wc,
+                            float(net._classification.normalization_multiplier[0]))
+    assert set(hip) == set(ref), (sorted(set(hip) ^ set(ref)))
+    for n in sorted(ref):
+        a, b = hip[n].double(), ref[n].double()
+        scale = b.abs().max().item() + 1e-12
+        err = (a - b).abs().max().item() / scale
+        assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"

@@ -20,6 +20,12 @@ from model_util import build_model
 from oracle import train_ref
 
 NAMES = train_golden_names()
+FINETUNE = [n for n in NAMES if n.startswith("train_finetune_")]
+
+
+def _loss_weights(meta):
+    """(align, tanh, class) weights of train.py:51-61 for the fixture's phase (epoch 1)."""
+    return {"pretrain": (0.5, 5.0, 0.0), "joint": (5.0, 2.0, 2.0), "finetune": (0.0, 0.0, 2.0)}[meta["phase"]]
 
 
 def _t(a):
@@ -35,9 +41,11 @@ def test_oracle_loss_terms_match_reference(name):
         proto = _t(rec[f"s{i}_proto"]) if f"s{i}_proto" in rec else torch.zeros(pooled.shape + (1, 1)) + 0.5
         got = train_ref.loss_terms(proto, pooled, out, ys, mult)
         assert float(got["tanh"]) == pytest.approx(comp["tanh"], rel=1e-5, abs=1e-6)
-        assert float(got["cls"]) == pytest.approx(comp["class"], rel=1e-5, abs=1e-6)
-        assert float(got["correct"]) / (2 * len(ys)) == comp["acc"]
-        assert comp["loss"] == pytest.approx(2.0 * comp["class"], rel=1e-6)   # finetune: loss = 2 * class
+        if meta["phase"] != "pretrain":
+            assert float(got["cls"]) == pytest.approx(comp["class"], rel=1e-5, abs=1e-6)
+            assert float(got["correct"]) / (2 * len(ys)) == comp["acc"]
+        wa, wt, wc = _loss_weights(meta)
+        assert comp["loss"] == pytest.approx(wa * comp["align"] + wt * comp["tanh"] + wc * comp["class"], rel=1e-5)
         if f"s{i}_proto" in rec:
             assert float(got["align"]) == pytest.approx(comp["align"], rel=1e-5, abs=1e-6)
 
@@ -51,7 +59,7 @@ def _initial_classifier(name):
     return meta, rec, w, b, float(cls.normalization_multiplier.detach()[0])
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", FINETUNE)
 def test_oracle_update_chain_matches_reference(name):
     meta, rec, w, b, mult = _initial_classifier(name)
     if "s0_w" in rec:
