@@ -29,15 +29,17 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "images/sec fwd, CUB-200 224×224 bs=64 ConvNeXt-tiny, 1/2/4/8 MI355X"
 PEAK_F32_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0
+PEAK_BF16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: BF16 dense matrix peak
 
 
-def make_net(device, num_classes=200):
-    from count_pipnet_amd.pipnet import get_pipnet
+def make_net(device, num_classes=200, precision="fp32"):
+    from count_pipnet_amd.pipnet import get_pipnet, set_hip_dtype
     from count_pipnet_amd.synthetic import fill_module_
     args = argparse.Namespace(net="convnext_tiny_26", disable_pretrained=True, num_features=0, bias=False)
     with contextlib.redirect_stdout(io.StringIO()):
         net, _ = get_pipnet(num_classes, args)
     fill_module_(net, 21, "trained")
+    set_hip_dtype(net, precision)
     return net.eval().to(device), args
 
 
@@ -98,6 +100,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
+                    help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
     a = ap.parse_args()
 
     from count_pipnet_amd import build, kernels
@@ -105,7 +109,7 @@ def main():
     rank, world, dev = init_from_env()
     build.build()
     from count_pipnet_amd.synthetic import synth_images
-    net, _ = make_net(dev)
+    net, _ = make_net(dev, precision=a.precision)
     # one process per GPU, weights resident, this rank's 64-image shard already in HBM; the
     # step ends with the RCCL all-gather of pooled + logits (DataParallel's gather)
     sharded = ShardedInference(net)
@@ -149,6 +153,10 @@ def main():
     gemm_flops = sum(v[1] for v in agg.values())
     gemm_time = sum(v[2] for v in agg.values())
 
+    split = a.precision == "bf16x3"
+    # split-bf16 GEMMs run 3 bf16 products per fp32 product: their fp32-equivalent ceiling is
+    # the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
+    peak = PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
     imgs = a.batch * world * a.steps
     ms = elapsed / a.steps * 1e3
     gflop_img = 40.094159616       # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
@@ -163,15 +171,15 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (bf16x3 split-product GEMMs)" if split else "f32",
         "data": "synthetic",
         "config": {"workload": "PIP-Net ConvNeXt-tiny-26 forward(inference=True), 224x224, 200 classes, fp32 "
-                               "(BASELINE configs[1]; configs[3] at N=8)",
+                               "(BASELINE configs[1]; configs[3] at N=8)" + (", split-bf16 GEMMs" if split else ""),
                    "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
                    "parallelism": f"dp{world}", "exchange": "rccl all_gather(logits, pooled)" if world > 1 else None},
         "roofline": {"bound": "mfma", "kernel": dom,
-                     "achieved": fl / tt / 1e12, "peak": PEAK_F32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": fl / tt / 1e12 / PEAK_F32_TFLOPS, "traffic": None,
+                     "achieved": fl / tt / 1e12, "peak": peak, "unit": "TFLOP/s",
+                     "frac": fl / tt / 1e12 / peak, "traffic": None,
                      "launches_per_step": n_l / a.steps, "avg_launch_us": tt / n_l * 1e6,
                      "algorithmic_gflop_per_launch": fl / n_l / 1e9},
         "model_tflops": gflop_img * a.batch * world / (ms * 1e-3) / 1e3 / world,

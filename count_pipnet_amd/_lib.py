@@ -34,6 +34,9 @@ SIGNATURES = {
     "pipnet_nchw_to_nhwc_f32": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_conv2d_nhwc_bf16": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, P],
     "pipnet_conv2d_nhwc_bf16_tile": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, I32, P],
+    "pipnet_conv2d_nhwc_s3": [P, I32, I32, I32, I32, P, P, P, P, I32, I32, I32, I32, I32, I32, P, I32, P],
+    "pipnet_dwconv7_ln_s3": [P, I32, I32, I32, I32, P, P, P, P, P, P],
+    "pipnet_layernorm_s3": [P, I64, I32, P, P, P, P],
     "pipnet_maxpool2d_nhwc_bf16": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_bf16": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_softmax_pool_bf16": [P, I32, I32, I32, I32, P, P, P],
@@ -75,6 +78,7 @@ _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, **_RESTYPE_EXTRA}
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
 EPI_RESID_ROWSCALE = 7
 EPI_GELU_BWD = 8
+EPI_S3_GELU, EPI_F32_BIAS, EPI_F32_RESID = 9, 10, 11      # split-bf16 ("bf16x3") ConvNeXt path
 
 _lib = None
 

@@ -120,7 +120,8 @@ class ConvNeXt(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         if use_hip(self):
-            return nhwc_as_nchw(convnext_features_hip(self.features, x, self._hip_pack))
+            return nhwc_as_nchw(convnext_features_hip(self.features, x, self._hip_pack,
+                                                      precision=getattr(self, "hip_precision", "fp32")))
         x = self.features(x)
         x = self.avgpool(x)
         return self.classifier(x)
@@ -170,7 +171,8 @@ class MidLayerConvNeXt(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         if use_hip(self):
-            return nhwc_as_nchw(convnext_features_hip(self.features, x, self._hip_pack))
+            return nhwc_as_nchw(convnext_features_hip(self.features, x, self._hip_pack,
+                                                      precision=getattr(self, "hip_precision", "fp32")))
         return self.features(x)
 
 
@@ -253,6 +255,27 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
     return h
 
 
+def _cnblock_s3(blk: CNBlock, h: Tensor, cache: Dict, key: str) -> Tensor:
+    """One CNBlock in place on NHWC fp32 ``h`` with split-bf16 GEMMs (precision "bf16x3"):
+    dwconv+LN writes split planes [hi|lo|hi], Linear1 (+GELU) reads them and writes its own
+    output as split planes, Linear2 adds layer_scale * (.) into the fp32 residual stream."""
+    dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
+    b, hh, ww, c = h.shape
+    if dw.kernel_size != (7, 7) or dw.padding != (3, 3) or dw.groups != c or dw.stride != (1, 1):
+        raise RuntimeError(f"CNBlock {key}: unsupported depthwise conv {dw}")
+    hid = l1.out_features
+    wdw = packed(cache, key + ".dw", dw.weight, lambda w: w.reshape(c, 49).t())
+    w1 = packed(cache, key + ".fc1.s3", l1.weight, lambda w: K.split_planes_weight(w.view(hid, 1, 1, c)))
+    w2 = packed(cache, key + ".fc2.s3", l2.weight, lambda w: K.split_planes_weight(w.view(c, 1, 1, hid)))
+    t3 = K.dwconv7_ln_s3(h, wdw, dw.bias, ln.weight, ln.bias)
+    u3 = K.conv_s3(t3, w1, 1, 1, hid, l1.bias, 1, 0, _lib.EPI_S3_GELU)
+    K.conv_s3(u3, w2, 1, 1, c, l2.bias, 1, 0, _lib.EPI_F32_RESID, scale=blk.layer_scale.view(-1), r=h, out=h)
+    return h
+
+
+PRECISIONS = ("fp32", "bf16x3")
+
+
 def stochastic_depth_row_scales(features: nn.Sequential, sd_keep: Dict[int, object], batch: int,
                                 device) -> Dict[int, Tensor]:
     """Per-block device vectors keep_b / (1 - p) (float32, as StochasticDepth's
@@ -273,10 +296,16 @@ def stochastic_depth_row_scales(features: nn.Sequential, sd_keep: Dict[int, obje
 
 
 def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
-                          sd_keep: Optional[Dict[int, object]] = None) -> Tensor:
+                          sd_keep: Optional[Dict[int, object]] = None, precision: str = "fp32") -> Tensor:
     """Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels.
     ``sd_keep``: train-mode stochastic depth, block id (0..17 in module order) -> per-sample
-    keep mask for every block with p > 0 (eval / None: no stochastic depth)."""
+    keep mask for every block with p > 0 (eval / None: no stochastic depth).
+    ``precision``: "fp32" (exact fp32 MFMA GEMMs) or "bf16x3" (the CNBlock Linears and the
+    downsample convs as split-bf16 GEMMs, include/pipnet_amd.h; inference only -- train-mode
+    stochastic depth always runs fp32)."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"unknown HIP precision {precision!r} (expected one of {PRECISIONS})")
+    s3 = precision == "bf16x3" and sd_keep is None
     K.require_device(x, "network input")
     x = x.contiguous()
     h = None
@@ -291,15 +320,24 @@ def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
             h = K.convnext_stem(x, conv.weight, conv.bias, ln.weight, ln.bias)
         elif len(mod) > 0 and isinstance(mod[0], CNBlock):
             for j, blk in enumerate(mod):
-                h = _cnblock_hip(blk, h, cache, f"{name}.{j}", None if scales is None else scales.get(bid))
+                if s3:
+                    h = _cnblock_s3(blk, h, cache, f"{name}.{j}")
+                else:
+                    h = _cnblock_hip(blk, h, cache, f"{name}.{j}", None if scales is None else scales.get(bid))
                 bid += 1
         elif len(mod) == 2 and isinstance(mod[0], LayerNorm2d) and isinstance(mod[1], nn.Conv2d):
             ln, conv = mod[0], mod[1]
             if conv.kernel_size != (2, 2) or conv.padding != (0, 0):
                 raise RuntimeError(f"unsupported ConvNeXt downsample {conv}")
-            t = K.layernorm(h, ln.weight, ln.bias)
-            wp = packed(cache, name + ".conv", conv.weight, lambda w: w.permute(0, 2, 3, 1))
-            h = K.conv2x2(t, wp, conv.bias, conv.stride[0])
+            if s3 and conv.in_channels % 32 == 0:
+                t3 = K.layernorm_s3(h, ln.weight, ln.bias)
+                wp = packed(cache, name + ".conv.s3", conv.weight,
+                            lambda w: K.split_planes_weight(w.permute(0, 2, 3, 1)))
+                h = K.conv_s3(t3, wp, 2, 2, conv.out_channels, conv.bias, conv.stride[0], 0, _lib.EPI_F32_BIAS)
+            else:
+                t = K.layernorm(h, ln.weight, ln.bias)
+                wp = packed(cache, name + ".conv", conv.weight, lambda w: w.permute(0, 2, 3, 1))
+                h = K.conv2x2(t, wp, conv.bias, conv.stride[0])
         else:
             raise RuntimeError(f"unsupported ConvNeXt features entry {idx}: {type(mod).__name__}")
     return h

@@ -31,9 +31,9 @@ using CfgN64 = Cfg<4, 1, 2, 2, 32, 4>; // 256 x 64 (N = 64 layers), BK 32 x 4 st
 // Mirrored by kernels.py:bf16_conv_tile.
 // N >= 256 layers run the ping-pong 16x16x32 kernel (tile 5) at every batch size -- the
 // choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
-int conv_variant(int M, int N, bool pp_ok) {
+int conv_variant(int M, int N, bool pp_ok, bool s3 = false) {
   if (N >= 256 && pp_ok) return 5;
-  if (N <= 64) return 6;          // 256 x 64: a 128-wide tile would compute half padding columns
+  if (N <= 64 && !s3) return 6;   // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
   if (N >= 256 && tl >= 256) return 3;
@@ -41,10 +41,14 @@ int conv_variant(int M, int N, bool pp_ok) {
   return 0;
 }
 
+bool is_s3_epi(int epi) {
+  return epi == PIPNET_EPI_S3_GELU || epi == PIPNET_EPI_F32_BIAS || epi == PIPNET_EPI_F32_RESID;
+}
+
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
-  if (v < 0) v = conv_variant(p.M, p.N, pp_ok);
+  if (v < 0) v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi));
   if (v > 6 || (v == 5 && !pp_ok)) return PIPNET_ERR_ARG;
   if (v == 5) {
     p.nt = (p.N + 255) / 256;
@@ -59,6 +63,15 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
         break;
       case PIPNET_EPI_BIAS_RESID_RELU:
         hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_BIAS_RESID_RELU, ALOAD>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_S3_GELU:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_S3_GELU, ALOAD>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_F32_BIAS:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_F32_BIAS, ALOAD>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_F32_RESID:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_F32_RESID, ALOAD>), grid, dim3(512), 0, s, p);
         break;
       default: return PIPNET_ERR_ARG;
     }
@@ -80,7 +93,17 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     else if (v == 1) hipLaunchKernelGGL((conv_bf16_kernel<CfgM, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p);        \
     break;
+  // split-bf16 epilogues: only the tiles the automatic choice picks for N < 256 (0 and 4)
+#define PIPNET_S3_CASE(E)                                                                            \
+  case E:                                                                                           \
+    if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
+    else if (v == 0) hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p); \
+    else return PIPNET_ERR_ARG;                                                                     \
+    break;
   switch (epi) {
+    PIPNET_S3_CASE(PIPNET_EPI_S3_GELU)
+    PIPNET_S3_CASE(PIPNET_EPI_F32_BIAS)
+    PIPNET_S3_CASE(PIPNET_EPI_F32_RESID)
     PIPNET_BF_CASE(PIPNET_EPI_NONE)
     PIPNET_BF_CASE(PIPNET_EPI_BIAS)
     PIPNET_BF_CASE(PIPNET_EPI_BIAS_RELU)
@@ -88,6 +111,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     default: return PIPNET_ERR_ARG;
   }
 #undef PIPNET_BF_CASE
+#undef PIPNET_S3_CASE
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }
@@ -214,4 +238,47 @@ extern "C" int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, in
                      reinterpret_cast<bf16*>(y));
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
+}
+
+// Split-bf16 ("bf16x3") conv / linear of the ConvNeXt backbone (include/pipnet_amd.h).
+extern "C" int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin3, const void* w_packed,
+                                     const float* bias, const float* scale, const float* R, int Cout, int KH, int KW,
+                                     int stride, int pad, int epilogue, void* y, int tile, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin3 <= 0 || (Cin3 % 32) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
+      stride <= 0 || pad < 0)
+    return PIPNET_ERR_ARG;
+  if (!is_s3_epi(epilogue)) return PIPNET_ERR_ARG;
+  if (epilogue == PIPNET_EPI_F32_RESID && (!R || !scale)) return PIPNET_ERR_ARG;
+  if (tile != -1 && tile != 0 && tile != 4 && tile != 5) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y) || (R && !aligned16(R)) || (bias && !aligned16(bias)) ||
+      (scale && !aligned16(scale)))
+    return PIPNET_ERR_ALIGN;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
+  if (OH <= 0 || OW <= 0) return PIPNET_ERR_ARG;
+  if ((int64_t)B * OH * OW >= (int64_t)1 << 31) return PIPNET_ERR_ARG;
+  if (B == 0) return PIPNET_OK;
+  ConvParams p{};
+  p.A = reinterpret_cast<const bf16*>(x);
+  p.W = reinterpret_cast<const bf16*>(w_packed);
+  p.bias = bias;
+  p.scale = scale;
+  p.R32 = R;
+  p.ldr = Cout;
+  if (epilogue == PIPNET_EPI_S3_GELU) {
+    p.C = reinterpret_cast<bf16*>(y);
+    p.ldc = 3 * (int64_t)Cout;
+  } else {
+    p.Cf = reinterpret_cast<float*>(y);
+    p.ldc = Cout;
+  }
+  p.M = B * OH * OW; p.N = Cout;
+  p.Kv = KH * KW * Cin3;
+  p.K = (p.Kv + KPAD - 1) / KPAD * KPAD;
+  p.H = H; p.Wd = W; p.Cin = Cin3; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
+    p.lda = Cin3;
+    return launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream);
+  }
+  return launch_conv<ALOAD_CONV>(p, epilogue, tile, (hipStream_t)stream);
 }

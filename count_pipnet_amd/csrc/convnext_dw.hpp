@@ -12,14 +12,15 @@ constexpr int DW_THREADS = 192;
 // once into registers (TX+6 float4) and feeds every output row it touches; the raw tile
 // then goes through LDS for the per-pixel LayerNorm (one wave per pixel, two-pass
 // mean / variance, coalesced NHWC stores).  1-D grid, XCD-contiguous, so the halo rows of
-// neighbouring workgroups are served from one L2.
-template <int C, int TX, int TY, int MINB>
+// neighbouring workgroups are served from one L2.  S3: the output is written as split-bf16
+// planes [hi | lo | hi] (3C bf16 per pixel, the A operand of the split-bf16 Linear1).
+template <int C, int TX, int TY, int MINB, bool S3 = false>
 __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
                                                                       const float* __restrict__ wp,
                                                                       const float* __restrict__ bias,
                                                                       const float* __restrict__ lnw,
                                                                       const float* __restrict__ lnb,
-                                                                      float* __restrict__ y) {
+                                                                      void* __restrict__ yv) {
   constexpr int QC = C / 4;
   constexpr int G = DW_THREADS / QC;
   constexpr int NP = G * TX;
@@ -95,21 +96,37 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
       qq = fmaf(d, d, qq);
     }
     const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
-    float* dst = y + (((int64_t)b * H + oy) * W + ox) * C;
+    const int64_t opix = ((int64_t)b * H + oy) * W + ox;
+    if constexpr (S3) {
+      __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 3 * C;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      if (c < C) dst[c] = (vv[j] - mean) * rstd * lnw[c] + lnb[c];
+      for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        if (c < C) {
+          __bf16 hi, lo;
+          split_bf16((vv[j] - mean) * rstd * lnw[c] + lnb[c], hi, lo);
+          dst[c] = hi;
+          dst[C + c] = lo;
+          dst[2 * C + c] = hi;
+        }
+      }
+    } else {
+      float* dst = reinterpret_cast<float*>(yv) + opix * C;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int c = lane + 64 * j;
+        if (c < C) dst[c] = (vv[j] - mean) * rstd * lnw[c] + lnb[c];
+      }
     }
   }
 }
 
-template <int C, int TX, int TY, int MINB>
+template <int C, int TX, int TY, int MINB, bool S3 = false>
 inline int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
-                     const float* lnb, float* y, hipStream_t s) {
+                     const float* lnb, void* y, hipStream_t s) {
   constexpr int NP = (DW_THREADS / (C / 4)) * TX;
   const dim3 grid(((W + NP - 1) / NP) * ((H + TY - 1) / TY) * B);
-  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX, TY, MINB>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw,
+  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX, TY, MINB, S3>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw,
                      lnb, y);
   return hipGetLastError() == hipSuccess ? PIPNET_OK : PIPNET_ERR_LAUNCH;
 }

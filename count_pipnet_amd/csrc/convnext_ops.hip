@@ -134,10 +134,10 @@ __global__ __launch_bounds__(STEM_T) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 // ---------------------------------------------------------------------------------------
 // row LayerNorm: one wave per row of C channels.
 // ---------------------------------------------------------------------------------------
-template <int NJ>
+template <int NJ, bool S3 = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int C,
                                                         const float* __restrict__ w, const float* __restrict__ b,
-                                                        float* __restrict__ y) {
+                                                        void* __restrict__ yv) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -159,11 +159,26 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     q = fmaf(d, d, q);
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + LN_EPS);
-  float* dst = y + row * C;
+  if constexpr (S3) {                      // split-bf16 planes [hi | lo | hi]
+    __bf16* dst = reinterpret_cast<__bf16*>(yv) + row * 3 * C;
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int c = lane + 64 * j;
-    if (c < C) dst[c] = (v[j] - mean) * rstd * w[c] + b[c];
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) {
+        __bf16 hi, lo;
+        split_bf16((v[j] - mean) * rstd * w[c] + b[c], hi, lo);
+        dst[c] = hi;
+        dst[C + c] = lo;
+        dst[2 * C + c] = hi;
+      }
+    }
+  } else {
+    float* dst = reinterpret_cast<float*>(yv) + row * C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < C) dst[c] = (v[j] - mean) * rstd * w[c] + b[c];
+    }
   }
 }
 
@@ -201,6 +216,38 @@ extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C,
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     default: return PIPNET_ERR_ARG;
   }
+}
+
+extern "C" int pipnet_dwconv7_ln_s3(const float* x, int B, int H, int W, int C, const float* w_packed,
+                                    const float* bias, const float* ln_w, const float* ln_b, void* y, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !bias || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (C) {
+    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 192: return pipnet_dw::launch_dw<192, 7, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 768: return pipnet_dw::launch_dw<768, 13, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    default: return PIPNET_ERR_ARG;
+  }
+}
+
+extern "C" int pipnet_layernorm_s3(const float* x, int64_t rows, int C, const float* w, const float* b, void* y,
+                                   void* stream) {
+  if (rows < 0 || C <= 0 || C > 2048 || !x || !w || !b || !y) return PIPNET_ERR_ARG;
+  if (rows == 0) return PIPNET_OK;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t s = (hipStream_t)stream;
+  const int nj = (C + 63) / 64;
+  if (nj <= 2) hipLaunchKernelGGL((layernorm_kernel<2, true>), grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 3) hipLaunchKernelGGL((layernorm_kernel<3, true>), grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 6) hipLaunchKernelGGL((layernorm_kernel<6, true>), grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else if (nj <= 12) hipLaunchKernelGGL((layernorm_kernel<12, true>), grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  else hipLaunchKernelGGL((layernorm_kernel<32, true>), grid, dim3(256), 0, s, x, rows, C, w, b, y);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
 }
 
 extern "C" int pipnet_layernorm_f32(const float* x, int64_t rows, int C, const float* w, const float* b, float* y,

@@ -36,6 +36,9 @@ struct ConvParams {
   int64_t ldr;
   bf16* C;
   int64_t ldc;
+  const float* scale;  // [N] layer scale (EPI_F32_RESID)
+  const float* R32;    // fp32 residual [M][ldr] (EPI_F32_RESID), may alias Cf
+  float* Cf;           // fp32 output [M][ldc] (EPI_F32_BIAS / EPI_F32_RESID)
   int M, N, K, Kv;
   int H, Wd, Cin, OH, OW, stride, KW, pad;
   int mt, nt, group_m;
@@ -163,6 +166,40 @@ PIPNET_DEV void tile_coords(const ConvParams& p, int bm, int bn, int& m0, int& n
 
 PIPNET_DEV u32x4 as_u32x4(const bf16x8& v) { return __builtin_bit_cast(u32x4, v); }
 
+// Epilogues of the split-bf16 ConvNeXt path (include/pipnet_amd.h, pipnet_conv2d_nhwc_s3):
+// x0 / x1 = accumulator + bias of channels n .. n+7 of row m.  S3_GELU writes GELU's output
+// as the next GEMM's A operand, split planes [hi | lo | hi] (row pitch ldc = 3N); F32_BIAS /
+// F32_RESID write fp32 (the residual stream and the downsample outputs stay fp32).
+template <int EPI>
+PIPNET_DEV void finish_s3(const ConvParams& p, int m, int n, f32x4 x0, f32x4 x1, f32x4 s0, f32x4 s1) {
+  if constexpr (EPI == PIPNET_EPI_S3_GELU) {
+    const f32x2 g0 = gelu_pk16(f32x2{x0[0], x0[1]}), g1 = gelu_pk16(f32x2{x0[2], x0[3]});
+    const f32x2 g2 = gelu_pk16(f32x2{x1[0], x1[1]}), g3 = gelu_pk16(f32x2{x1[2], x1[3]});
+    const float g[8] = {g0[0], g0[1], g1[0], g1[1], g2[0], g2[1], g3[0], g3[1]};
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bf16 h, l;
+      split_bf16(g[e], h, l);
+      hi[e] = h;
+      lo[e] = l;
+    }
+    bf16* dst = p.C + (int64_t)m * p.ldc + n;
+    *reinterpret_cast<bf16x8*>(dst) = hi;
+    *reinterpret_cast<bf16x8*>(dst + p.N) = lo;
+    *reinterpret_cast<bf16x8*>(dst + 2 * p.N) = hi;
+  } else {
+    if constexpr (EPI == PIPNET_EPI_F32_RESID) {
+      const float* r = p.R32 + (int64_t)m * p.ldr + n;
+      x0 = ld4(r) + s0 * x0;
+      x1 = ld4(r + 4) + s1 * x1;
+    }
+    float* dst = p.Cf + (int64_t)m * p.ldc + n;
+    st4(dst, x0);
+    st4(dst + 4, x1);
+  }
+}
+
 // Epilogue: each wave re-lays its 32 x (TN*32) fp32 accumulator slice through LDS (rows
 // padded by 4 floats: the 16-B reads of one row's lanes then cover all 64 banks), then every
 // lane finishes 8 consecutive channels of one pixel -- bias, residual (one 16-B bf16
@@ -180,10 +217,14 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
   const int c8 = lane % CPR;
   const int n = n0 + wn * 32 * TN + 8 * c8;
   const bool nok = n < p.N;
-  f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, s0 = b0, s1 = b0;
   if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
     b0 = ld4(p.bias + n);
     b1 = ld4(p.bias + n + 4);
+  }
+  if (EPI == PIPNET_EPI_F32_RESID && nok) {
+    s0 = ld4(p.scale + n);
+    s1 = ld4(p.scale + n + 4);
   }
   bf16x8 r[TM][NIT];
   if (HAS_R) {
@@ -210,6 +251,10 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
       f32x4 x0 = ld4(wt + row * LD + 8 * c8), x1 = ld4(wt + row * LD + 8 * c8 + 4);
       x0 += b0;
       x1 += b1;
+      if constexpr (EPI >= PIPNET_EPI_S3_GELU) {
+        if (m < p.M && nok) finish_s3<EPI>(p, m, n, x0, x1, s0, s1);
+        continue;
+      }
       if (HAS_R) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -518,10 +563,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   const int c8 = lane & 7;
   const int n = n0 + wc * 64 + 8 * c8;
   const bool nok = n < p.N;
-  f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+  f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, s0 = b0, s1 = b0;
   if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
     b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
     b1 = *reinterpret_cast<const f32x4v*>(p.bias + n + 4);
+  }
+  if (EPI == PIPNET_EPI_F32_RESID && nok) {
+    s0 = *reinterpret_cast<const f32x4v*>(p.scale + n);
+    s1 = *reinterpret_cast<const f32x4v*>(p.scale + n + 4);
   }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -549,6 +598,10 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
       f32x4v x1 = *reinterpret_cast<const f32x4v*>(wt + row * EPI_LD + 8 * c8 + 4);
       x0 += b0;
       x1 += b1;
+      if constexpr (EPI >= PIPNET_EPI_S3_GELU) {
+        if (m < p.M && nok) finish_s3<EPI>(p, m, n, x0, x1, s0, s1);
+        continue;
+      }
       if (HAS_R) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

@@ -234,10 +234,23 @@ def get_pip_network(num_classes: int, args: argparse.Namespace):
 
 
 def set_hip_dtype(model: nn.Module, dtype) -> nn.Module:
-    """Select the compute dtype of the HIP inference path: torch.float32 (default, exact
-    parity with the reference) or torch.bfloat16 (the BASELINE C3 ResNet build).  bf16 is
-    implemented for the ResNet backbones only."""
+    """Select the compute dtype of the HIP inference path:
+      * torch.float32 / "fp32" (default): exact fp32 arithmetic, parity with the reference;
+      * torch.bfloat16 / "bf16": the BASELINE C3 ResNet build (bf16 activations);
+      * "bf16x3": ConvNeXt backbones -- fp32 activations, the CNBlock Linears and downsample
+        convs as split-bf16 GEMMs (x = hi + lo, three bf16 products, fp32 accumulation;
+        ~1e-5 relative per product, include/pipnet_amd.h pipnet_conv2d_nhwc_s3)."""
+    from .convnext_features import ConvNeXt, MidLayerConvNeXt
     from .resnet_features import ResNet_features
+    if dtype in ("bf16x3", "split_bf16"):
+        found = False
+        for m in model.modules():
+            if isinstance(m, (ConvNeXt, MidLayerConvNeXt)):
+                m.hip_precision = "bf16x3"
+                found = True
+        if not found:
+            raise ValueError("the bf16x3 HIP path is implemented for ConvNeXt backbones only")
+        return model
     dtype = {"fp32": torch.float32, "f32": torch.float32, "bf16": torch.bfloat16}.get(dtype, dtype)
     if dtype not in (torch.float32, torch.bfloat16):
         raise ValueError(f"unsupported HIP compute dtype {dtype}")
@@ -246,6 +259,8 @@ def set_hip_dtype(model: nn.Module, dtype) -> nn.Module:
         if isinstance(m, ResNet_features):
             m.hip_dtype = dtype
             found = True
+        if dtype == torch.float32 and isinstance(m, (ConvNeXt, MidLayerConvNeXt)):
+            m.hip_precision = "fp32"
     if dtype == torch.bfloat16 and not found:
         raise ValueError("the bf16 HIP path is implemented for ResNet backbones only")
     return model
@@ -253,7 +268,7 @@ def set_hip_dtype(model: nn.Module, dtype) -> nn.Module:
 
 def get_pipnet(num_classes: int, args: argparse.Namespace):
     """pipnet.py:117-139 -> (PIPNet, num_prototypes).  Optional ``args.hip_dtype``
-    ("fp32" | "bf16") selects the HIP compute dtype (see set_hip_dtype)."""
+    ("fp32" | "bf16" | "bf16x3") selects the HIP compute dtype (see set_hip_dtype)."""
     feature_net, add_on, pool, classification, num_prototypes = get_pip_network(num_classes, args)
     model = PIPNet(num_classes=num_classes, num_prototypes=num_prototypes, feature_net=feature_net, args=args,
                    add_on_layers=add_on, pool_layer=pool, classification_layer=classification)

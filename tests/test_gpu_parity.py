@@ -50,8 +50,25 @@ def _near_tie_images(meta, rec, margin=TOL):
 
 @pytest.mark.parametrize("name", HIP_CASES)
 def test_hip_forward_matches_reference_golden(gpu, name):
+    _golden_case(gpu, name)
+
+
+SPLIT_CASES = [n for n in HIP_CASES if "resnet" not in n]
+
+
+@pytest.mark.parametrize("name", SPLIT_CASES)
+def test_hip_bf16x3_forward_matches_reference_golden(gpu, name):
+    """The split-bf16 ConvNeXt build (set_hip_dtype(net, "bf16x3")) against the same
+    reference goldens at the same 1e-3 tolerance (north star) as the exact-fp32 build."""
+    _golden_case(gpu, name, precision="bf16x3")
+
+
+def _golden_case(gpu, name, precision=None):
     meta, rec = load_golden(name)
     net = build_model(meta).to(gpu)
+    if precision is not None:
+        from count_pipnet_amd.pipnet import set_hip_dtype
+        set_hip_dtype(net, precision)
     xs = golden_inputs(meta).to(gpu)
     count = meta["case"]["model"] == "count_pipnet"
     gumbel = count and meta["case"]["activation"] == "gumbel_softmax"
@@ -78,12 +95,14 @@ def test_hip_forward_matches_reference_golden(gpu, name):
             assert np.all(np.abs(proto[ok] - rec[tag + "_proto"][ok]) <= TOL)
 
 
-def test_c2_full_batch_properties(gpu):
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+def test_c2_full_batch_properties(gpu, precision):
     """C2 at its BASELINE size (bs=64, 224x224): softmax rows sum to 1, pooled is the
     spatial max of proto, logits are the NonNegLinear of the clamped pooled vector,
     results are batch-invariant (bitwise), and two images match the oracle."""
+    from count_pipnet_amd.pipnet import set_hip_dtype
     meta, _ = load_golden("c2_pipnet_convnext26")
-    net = build_model(meta).to(gpu)
+    net = set_hip_dtype(build_model(meta).to(gpu), precision)
     from count_pipnet_amd.synthetic import synth_images
     xs = synth_images(64, 224, seed=7).to(gpu)
     with torch.no_grad():
