@@ -102,6 +102,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
                     help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
+    ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
+                    help="also time this precision on the same network (reported under alt_precision)")
     a = ap.parse_args()
 
     from count_pipnet_amd import build, kernels
@@ -124,42 +126,51 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(a.warmup):
-        step()
-    # dominant-kernel roofline: inside the timed region every MFMA GEMM launch is bracketed
-    # by HIP events recorded on the stream it is launched on (torch's current stream).
-    timer = GemmTimer()
-    kernels.set_launch_hook(timer)
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    timer.enabled = True
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    timer.enabled = False
-    kernels.set_launch_hook(None)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    agg = timer.summary()
-    dom = max(agg, key=lambda k: agg[k][2])
-    n_l, fl, tt = agg[dom]
+    def timed():
+        """W warm-up steps, then K steps bracketed by barrier + synchronize; every MFMA GEMM
+        launch in the timed region is bracketed by HIP events on the stream it is launched
+        on (torch's current stream) for the dominant-kernel roofline.  Max over ranks."""
+        for _ in range(a.warmup):
+            step()
+        timer = GemmTimer()
+        kernels.set_launch_hook(timer)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        timer.enabled = True
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        timer.enabled = False
+        kernels.set_launch_hook(None)
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return elapsed, timer.summary()
+
+    def roofline(agg, split):
+        dom = max(agg, key=lambda k: agg[k][2])
+        n_l, fl, tt = agg[dom]
+        # split-bf16 GEMMs run 3 bf16 products per fp32 product: their fp32-equivalent ceiling
+        # is the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
+        peak = PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
+        return dom, {"bound": "mfma", "kernel": dom, "achieved": fl / tt / 1e12, "peak": peak, "unit": "TFLOP/s",
+                     "frac": fl / tt / 1e12 / peak, "traffic": None, "launches_per_step": n_l / a.steps,
+                     "avg_launch_us": tt / n_l * 1e6, "algorithmic_gflop_per_launch": fl / n_l / 1e9}
+
+    gflop_img = 40.094159616       # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
+    elapsed, agg = timed()
+    split = a.precision == "bf16x3"
+    dom, roof = roofline(agg, split)
     gemm_flops = sum(v[1] for v in agg.values())
     gemm_time = sum(v[2] for v in agg.values())
-
-    split = a.precision == "bf16x3"
-    # split-bf16 GEMMs run 3 bf16 products per fp32 product: their fp32-equivalent ceiling is
-    # the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
-    peak = PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
     imgs = a.batch * world * a.steps
     ms = elapsed / a.steps * 1e3
-    gflop_img = 40.094159616       # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
     result = {
         "metric": METRIC,
         "value": imgs / elapsed,
@@ -177,15 +188,26 @@ def main():
                                "(BASELINE configs[1]; configs[3] at N=8)" + (", split-bf16 GEMMs" if split else ""),
                    "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
                    "parallelism": f"dp{world}", "exchange": "rccl all_gather(logits, pooled)" if world > 1 else None},
-        "roofline": {"bound": "mfma", "kernel": dom,
-                     "achieved": fl / tt / 1e12, "peak": peak, "unit": "TFLOP/s",
-                     "frac": fl / tt / 1e12 / peak, "traffic": None,
-                     "launches_per_step": n_l / a.steps, "avg_launch_us": tt / n_l * 1e6,
-                     "algorithmic_gflop_per_launch": fl / n_l / 1e9},
+        "roofline": roof,
         "model_tflops": gflop_img * a.batch * world / (ms * 1e-3) / 1e3 / world,
         "model_frac_of_f32_peak": gflop_img * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,
         "gemm_all": {"tflops": gemm_flops / gemm_time / 1e12, "ms_per_step": gemm_time / a.steps * 1e3},
     }
+    if a.alt_precision != "none" and a.alt_precision != a.precision:
+        # the same network and inputs with the other GEMM precision, timed the same way
+        from count_pipnet_amd.pipnet import set_hip_dtype
+        set_hip_dtype(net, a.alt_precision)
+        el2, agg2 = timed()
+        _, roof2 = roofline(agg2, a.alt_precision == "bf16x3")
+        ms2 = el2 / a.steps * 1e3
+        result["alt_precision"] = {
+            "precision": a.alt_precision,
+            "dtype": "f32 (bf16x3 split-product GEMMs)" if a.alt_precision == "bf16x3" else "f32",
+            "value": imgs / el2, "ms_per_step": ms2, "roofline": roof2,
+            "model_tflops_f32_equivalent": gflop_img * a.batch / (ms2 * 1e-3) / 1e3,
+            "accuracy": "fp32 inputs/outputs and accumulation; products of hi+lo bf16 splits (~1e-5 relative "
+                        "per product); parity vs the reference goldens at the north-star 1e-3 "
+                        "(tests/test_gpu_parity.py::test_hip_bf16x3_*)" if a.alt_precision == "bf16x3" else "exact"}
     traffic_path = os.path.join(REPO, "profiles", "traffic_latest.json")
     if os.path.exists(traffic_path):
         with open(traffic_path) as f:

@@ -257,7 +257,7 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
 
 def _cnblock_s3(blk: CNBlock, h: Tensor, cache: Dict, key: str) -> Tensor:
     """One CNBlock in place on NHWC fp32 ``h`` with split-bf16 GEMMs (precision "bf16x3"):
-    dwconv+LN writes split planes [hi|lo|hi], Linear1 (+GELU) reads them and writes its own
+    dwconv+LN writes split planes [hi|lo], Linear1 (+GELU) reads them and writes its own
     output as split planes, Linear2 adds layer_scale * (.) into the fp32 residual stream."""
     dw, ln, l1, l2 = blk.block[0], blk.block[2], blk.block[3], blk.block[5]
     b, hh, ww, c = h.shape

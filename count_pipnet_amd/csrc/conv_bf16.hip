@@ -33,6 +33,7 @@ using CfgN64 = Cfg<4, 1, 2, 2, 32, 4>; // 256 x 64 (N = 64 layers), BK 32 x 4 st
 // choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
 int conv_variant(int M, int N, bool pp_ok, bool s3 = false) {
   if (N >= 256 && pp_ok) return 5;
+  if (s3 && N >= 192 && pp_ok) return 5;   // split GEMMs: the ping-pong tile wins from N = 192 (tools/s3_tiles.py)
   if (N <= 64 && !s3) return 6;   // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
@@ -199,6 +200,8 @@ extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, 
   p.Kv = KH * KW * Cin;
   p.K = (p.Kv + KPAD - 1) / KPAD * KPAD;
   p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  p.Cinp = Cin;
+  p.seg = 0;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
     p.lda = Cin;
     return launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream);
@@ -240,11 +243,13 @@ extern "C" int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, in
   return PIPNET_OK;
 }
 
-// Split-bf16 ("bf16x3") conv / linear of the ConvNeXt backbone (include/pipnet_amd.h).
-extern "C" int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin3, const void* w_packed,
+// Split-bf16 ("bf16x3") conv / linear of the ConvNeXt backbone (include/pipnet_amd.h): x holds
+// split planes [hi | lo] (2 Cin channels per pixel), read as the virtual 3 Cin channels
+// [hi | lo | hi] of each tap (seg_remap), against weights [hi | hi | lo] per tap.
+extern "C" int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin, const void* w_packed,
                                      const float* bias, const float* scale, const float* R, int Cout, int KH, int KW,
                                      int stride, int pad, int epilogue, void* y, int tile, void* stream) {
-  if (B < 0 || H <= 0 || W <= 0 || Cin3 <= 0 || (Cin3 % 32) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || (Cin % 32) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
       stride <= 0 || pad < 0)
     return PIPNET_ERR_ARG;
   if (!is_s3_epi(epilogue)) return PIPNET_ERR_ARG;
@@ -267,17 +272,19 @@ extern "C" int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin
   p.ldr = Cout;
   if (epilogue == PIPNET_EPI_S3_GELU) {
     p.C = reinterpret_cast<bf16*>(y);
-    p.ldc = 3 * (int64_t)Cout;
+    p.ldc = 2 * (int64_t)Cout;
   } else {
     p.Cf = reinterpret_cast<float*>(y);
     p.ldc = Cout;
   }
   p.M = B * OH * OW; p.N = Cout;
-  p.Kv = KH * KW * Cin3;
-  p.K = (p.Kv + KPAD - 1) / KPAD * KPAD;
-  p.H = H; p.Wd = W; p.Cin = Cin3; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  p.Kv = KH * KW * 3 * Cin;
+  p.K = (p.Kv + 31) / 32 * 32;                 // the split tiles (0, 4, 5) all walk K in 32-deep steps
+  p.H = H; p.Wd = W; p.Cin = 3 * Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
+  p.Cinp = 2 * Cin;
+  p.seg = Cin;
   if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {
-    p.lda = Cin3;
+    p.lda = 2 * Cin;
     return launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream);
   }
   return launch_conv<ALOAD_CONV>(p, epilogue, tile, (hipStream_t)stream);

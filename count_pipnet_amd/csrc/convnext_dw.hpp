@@ -13,7 +13,7 @@ constexpr int DW_THREADS = 192;
 // then goes through LDS for the per-pixel LayerNorm (one wave per pixel, two-pass
 // mean / variance, coalesced NHWC stores).  1-D grid, XCD-contiguous, so the halo rows of
 // neighbouring workgroups are served from one L2.  S3: the output is written as split-bf16
-// planes [hi | lo | hi] (3C bf16 per pixel, the A operand of the split-bf16 Linear1).
+// planes [hi | lo] (2C bf16 per pixel, the A operand of the split-bf16 Linear1).
 template <int C, int TX, int TY, int MINB, bool S3 = false>
 __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
                                                                       const float* __restrict__ wp,
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
     const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
     const int64_t opix = ((int64_t)b * H + oy) * W + ox;
     if constexpr (S3) {
-      __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 3 * C;
+      __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 2 * C;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int c = lane + 64 * j;
@@ -107,7 +107,6 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
           split_bf16((vv[j] - mean) * rstd * lnw[c] + lnb[c], hi, lo);
           dst[c] = hi;
           dst[C + c] = lo;
-          dst[2 * C + c] = hi;
         }
       }
     } else {

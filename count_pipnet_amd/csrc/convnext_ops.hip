@@ -159,8 +159,8 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     q = fmaf(d, d, q);
   }
   const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + LN_EPS);
-  if constexpr (S3) {                      // split-bf16 planes [hi | lo | hi]
-    __bf16* dst = reinterpret_cast<__bf16*>(yv) + row * 3 * C;
+  if constexpr (S3) {                      // split-bf16 planes [hi | lo]
+    __bf16* dst = reinterpret_cast<__bf16*>(yv) + row * 2 * C;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = lane + 64 * j;
@@ -169,7 +169,6 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
         split_bf16((v[j] - mean) * rstd * w[c] + b[c], hi, lo);
         dst[c] = hi;
         dst[C + c] = lo;
-        dst[2 * C + c] = hi;
       }
     }
   } else {

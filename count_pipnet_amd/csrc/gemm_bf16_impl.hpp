@@ -41,10 +41,16 @@ struct ConvParams {
   float* Cf;           // fp32 output [M][ldc] (EPI_F32_BIAS / EPI_F32_RESID)
   int M, N, K, Kv;
   int H, Wd, Cin, OH, OW, stride, KW, pad;
+  int Cinp;            // physical channels per pixel of A (= Cin, or 2 seg for split planes)
+  int seg;             // split planes [hi | lo] of seg channels read as K' = [hi | lo | hi]: a
+                       // (virtual) channel c >= 2 seg is read at c - 2 seg; 0 = no remap
   int mt, nt, group_m;
 };
 
 enum { ALOAD_DENSE = 0, ALOAD_CONV = 2 };
+
+// virtual split-plane channel -> physical (K-tiles never straddle a segment: seg % 32 == 0)
+PIPNET_DEV int seg_remap(const ConvParams& p, int c) { return (p.seg && c >= 2 * p.seg) ? c - 2 * p.seg : c; }
 
 static __device__ __attribute__((aligned(16))) float g_zero_bf[4] = {0.f, 0.f, 0.f, 0.f};
 
@@ -65,7 +71,7 @@ PIPNET_DEV ARow a_row(const ConvParams& p, int m) {
   const int rr = m - b * ohw;
   const int oy = rr / p.OW;
   const int ox = rr - oy * p.OW;
-  r.base = (int64_t)b * p.H * p.Wd * p.Cin;
+  r.base = (int64_t)b * p.H * p.Wd * p.Cinp;
   r.iy0 = oy * p.stride - p.pad;
   r.ix0 = ox * p.stride - p.pad;
   return r;
@@ -75,14 +81,14 @@ PIPNET_DEV ARow a_row(const ConvParams& p, int m) {
 template <int ALOAD>
 PIPNET_DEV const void* a_ptr(const ConvParams& p, const ARow& r, int k) {
   if (k >= p.Kv) return g_zero_bf;   // K padding (packed weights are zero there too)
-  if (ALOAD == ALOAD_DENSE) return p.A + r.base + k;
+  if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k);
   const int tap = k / p.Cin;
   const int c = k - tap * p.Cin;
   const int ky = tap / p.KW;
   const int iy = r.iy0 + ky;
   const int ix = r.ix0 + tap - ky * p.KW;
   if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
-  return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + c;
+  return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, c);
 }
 
 // Workgroup tile: WGM x WGN waves, each wave TM x TN MFMA 32x32 tiles, BK-deep K tiles in NS
@@ -168,7 +174,7 @@ PIPNET_DEV u32x4 as_u32x4(const bf16x8& v) { return __builtin_bit_cast(u32x4, v)
 
 // Epilogues of the split-bf16 ConvNeXt path (include/pipnet_amd.h, pipnet_conv2d_nhwc_s3):
 // x0 / x1 = accumulator + bias of channels n .. n+7 of row m.  S3_GELU writes GELU's output
-// as the next GEMM's A operand, split planes [hi | lo | hi] (row pitch ldc = 3N); F32_BIAS /
+// as the next GEMM's A operand, split planes [hi | lo] (row pitch ldc = 2N); F32_BIAS /
 // F32_RESID write fp32 (the residual stream and the downsample outputs stay fp32).
 template <int EPI>
 PIPNET_DEV void finish_s3(const ConvParams& p, int m, int n, f32x4 x0, f32x4 x1, f32x4 s0, f32x4 s1) {
@@ -187,7 +193,6 @@ PIPNET_DEV void finish_s3(const ConvParams& p, int m, int n, f32x4 x0, f32x4 x1,
     bf16* dst = p.C + (int64_t)m * p.ldc + n;
     *reinterpret_cast<bf16x8*>(dst) = hi;
     *reinterpret_cast<bf16x8*>(dst + p.N) = lo;
-    *reinterpret_cast<bf16x8*>(dst + 2 * p.N) = hi;
   } else {
     if constexpr (EPI == PIPNET_EPI_F32_RESID) {
       const float* r = p.R32 + (int64_t)m * p.ldr + n;
@@ -457,10 +462,10 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   int d_c = 0, d_kx = 0, d_ky = 0;
   auto a_src = [&](const ARow& r, int k0) -> const void* {
     if (k0 >= p.Kv) return g_zero_bf;
-    if (ALOAD == ALOAD_DENSE) return p.A + r.base + k0 + dchunk;
+    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k0) + dchunk;
     const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
     if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
-    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + d_c + dchunk;
+    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, d_c) + dchunk;
   };
   auto advance = [&]() {
     if (ALOAD != ALOAD_DENSE) {

@@ -192,7 +192,7 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False) -> int:
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
     MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
-    if n >= 256 and pp_ok:
+    if (n >= 256 or (s3 and n >= 192)) and pp_ok:
         return 5
     if n <= 64 and not s3:
         return 6
@@ -317,44 +317,46 @@ def dwconv7_ln(x_nhwc: Tensor, w_packed: Tensor, bias: Tensor, ln_w: Tensor, ln_
 
 
 # ---- split-bf16 ("bf16x3") ConvNeXt path (include/pipnet_amd.h, pipnet_conv2d_nhwc_s3) ----
+S3_KTILE = 32          # split weights: K padded to the 32-deep K tiles of the split kernels
 def split_planes_weight(w_ohwi: Tensor) -> Tensor:
     """fp32 weight [Cout, KH, KW, Cin] -> packed split-bf16 B operand [Cout, Kp] bf16: per tap
-    [hi | hi | lo] over 3 Cin (hi = RNE(w), lo = RNE(w - hi)), Kp = KH*KW*3Cin rounded up to 64."""
+    [hi | hi | lo] over 3 Cin (hi = RNE(w), lo = RNE(w - hi)), Kp = KH*KW*3Cin rounded up to 32."""
     hi = w_ohwi.to(torch.bfloat16)
     lo = (w_ohwi - hi.float()).to(torch.bfloat16)
     cout, kh, kw, cin = w_ohwi.shape
     k = kh * kw * 3 * cin
-    kp = -(-k // BF16_KTILE) * BF16_KTILE
+    kp = -(-k // S3_KTILE) * S3_KTILE
     out = torch.zeros((cout, kp), device=w_ohwi.device, dtype=torch.bfloat16)
     out[:, :k] = torch.cat([hi, hi, lo], dim=-1).reshape(cout, k)
     return out
 
 
 def split_planes(x: Tensor) -> Tensor:
-    """fp32 [..., C] -> split planes [..., 3C] bf16 [hi | lo | hi] (what the producer kernels
+    """fp32 [..., C] -> split planes [..., 2C] bf16 [hi | lo] (what the producer kernels
     write; for tests and for inputs that do not come from a split-writing kernel)."""
     hi = x.to(torch.bfloat16)
     lo = (x - hi.float()).to(torch.bfloat16)
-    return torch.cat([hi, lo, hi], dim=-1).contiguous()
+    return torch.cat([hi, lo], dim=-1).contiguous()
 
 
-def conv_s3(x3: Tensor, w_packed: Tensor, kh: int, kw: int, cout: int, bias: Optional[Tensor], stride: int, pad: int,
+def conv_s3(x2: Tensor, w_packed: Tensor, kh: int, kw: int, cout: int, bias: Optional[Tensor], stride: int, pad: int,
             epilogue: int, scale: Optional[Tensor] = None, r: Optional[Tensor] = None, out: Optional[Tensor] = None,
             tile: int = -1) -> Tensor:
-    """Split-bf16 conv / linear: x3 [B,H,W,3Cin] split planes, w_packed from split_planes_weight.
-    EPI_S3_GELU -> split planes [B,OH,OW,3Cout] of gelu(conv + b); EPI_F32_BIAS -> fp32
+    """Split-bf16 conv / linear: x2 [B,H,W,2Cin] split planes, w_packed from split_planes_weight.
+    EPI_S3_GELU -> split planes [B,OH,OW,2Cout] of gelu(conv + b); EPI_F32_BIAS -> fp32
     [B,OH,OW,Cout]; EPI_F32_RESID -> fp32 r + scale * (conv + b) (``out`` may be ``r``)."""
-    _chk_bf(x3, "split-plane input")
+    _chk_bf(x2, "split-plane input")
     _chk_bf(w_packed, "split-plane weight")
     if bias is not None:
         _chk(bias, "bias")
-    b, h, w, cin3 = x3.shape
-    k = kh * kw * cin3
-    if w_packed.shape[0] != cout or w_packed.shape[1] != -(-k // BF16_KTILE) * BF16_KTILE:
-        raise RuntimeError(f"conv_s3: packed weight {tuple(w_packed.shape)} does not match {kh}x{kw}x{cin3} -> {cout}")
+    b, h, w, cin2 = x2.shape
+    cin = cin2 // 2
+    k = kh * kw * 3 * cin
+    if cin2 % 2 or w_packed.shape[0] != cout or w_packed.shape[1] != -(-k // S3_KTILE) * S3_KTILE:
+        raise RuntimeError(f"conv_s3: packed weight {tuple(w_packed.shape)} does not match {kh}x{kw}x3*{cin} -> {cout}")
     oh, ow = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
     if epilogue == _lib.EPI_S3_GELU:
-        shape, dt = (b, oh, ow, 3 * cout), torch.bfloat16
+        shape, dt = (b, oh, ow, 2 * cout), torch.bfloat16
     else:
         shape, dt = (b, oh, ow, cout), torch.float32
     if epilogue == _lib.EPI_F32_RESID:
@@ -365,33 +367,33 @@ def conv_s3(x3: Tensor, w_packed: Tensor, kh: int, kw: int, cout: int, bias: Opt
         if r.numel() != b * oh * ow * cout:
             raise RuntimeError(f"conv_s3: residual {tuple(r.shape)} does not match {(b, oh, ow, cout)}")
     if out is None:
-        out = torch.empty(shape, device=x3.device, dtype=dt)
+        out = torch.empty(shape, device=x2.device, dtype=dt)
     elif out.dtype != dt or out.numel() != b * oh * ow * shape[-1] or not out.is_contiguous():
         raise RuntimeError(f"conv_s3: out {tuple(out.shape)} {out.dtype} does not match {shape} {dt}")
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
     _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, True, s3=True), 2.0 * m * cout * k / 3.0,
-            lambda: _lib.call("pipnet_conv2d_nhwc_s3", x3.data_ptr(), b, h, w, cin3, w_packed.data_ptr(), _ptr(bias),
+            lambda: _lib.call("pipnet_conv2d_nhwc_s3", x2.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
                               _ptr(scale), _ptr(r), cout, kh, kw, stride, pad, epilogue, out.data_ptr(), tile,
-                              _stream(x3)))
+                              _stream(x2)))
     return out
 
 
 def dwconv7_ln_s3(x_nhwc: Tensor, w_packed: Tensor, bias: Tensor, ln_w: Tensor, ln_b: Tensor) -> Tensor:
-    """pipnet_dwconv7_ln_f32 writing split planes [B,H,W,3C] bf16."""
+    """pipnet_dwconv7_ln_f32 writing split planes [B,H,W,2C] bf16."""
     _chk(x_nhwc, "dwconv input")
     b, h, w, c = x_nhwc.shape
-    y = torch.empty((b, h, w, 3 * c), device=x_nhwc.device, dtype=torch.bfloat16)
+    y = torch.empty((b, h, w, 2 * c), device=x_nhwc.device, dtype=torch.bfloat16)
     _lib.call("pipnet_dwconv7_ln_s3", x_nhwc.data_ptr(), b, h, w, c, w_packed.data_ptr(), bias.data_ptr(),
               ln_w.data_ptr(), ln_b.data_ptr(), y.data_ptr(), _stream(x_nhwc))
     return y
 
 
 def layernorm_s3(x: Tensor, w: Tensor, b: Tensor) -> Tensor:
-    """Row LayerNorm writing split planes [..., 3C] bf16."""
+    """Row LayerNorm writing split planes [..., 2C] bf16."""
     _chk(x, "layernorm input")
     c = x.shape[-1]
-    y = torch.empty(tuple(x.shape[:-1]) + (3 * c,), device=x.device, dtype=torch.bfloat16)
+    y = torch.empty(tuple(x.shape[:-1]) + (2 * c,), device=x.device, dtype=torch.bfloat16)
     _lib.call("pipnet_layernorm_s3", x.data_ptr(), x.numel() // c, c, w.data_ptr(), b.data_ptr(), y.data_ptr(),
               _stream(x))
     return y

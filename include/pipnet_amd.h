@@ -42,7 +42,7 @@ extern "C" {
                                         CNBlock Linear2 with train-mode stochastic depth)              */
 #define PIPNET_EPI_GELU_BWD 8        /* C = (A W^T) * gelu_erf'(R)   (training: d pre-GELU activation) */
 /* split-bf16 ("bf16x3") epilogues of pipnet_conv2d_nhwc_s3 (fp32 results, see there) */
-#define PIPNET_EPI_S3_GELU 9         /* g = gelu_erf(A W^T + b) stored as split planes [hi|lo|hi] bf16 */
+#define PIPNET_EPI_S3_GELU 9         /* g = gelu_erf(A W^T + b) stored as split planes [hi|lo] bf16    */
 #define PIPNET_EPI_F32_BIAS 10       /* C = A W^T + b, fp32                                            */
 #define PIPNET_EPI_F32_RESID 11      /* C = R + s * (A W^T + b), fp32 C and R (R may alias C)          */
 
@@ -129,27 +129,29 @@ int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, co
  * An fp32 operand x is carried as two bf16 values, hi = RNE(x) and lo = RNE(x - hi)
  * (x = hi + lo to ~2^-17 relative).  A product x.w is then hi.hi + lo.hi + hi.lo (the
  * lo.lo term, ~2^-16 relative, is dropped), accumulated in fp32 -- a bf16 GEMM over K' = 3K
- * whose A rows are the "split planes" [hi(x) | lo(x) | hi(x)] (3 Cin bf16 per pixel) and
- * whose weight rows are [hi(w) | hi(w) | lo(w)] per tap.  Per-product error ~1e-5
- * relative (fp32: 6e-8) at 3/16 of the fp32-MFMA cost (v_mfma_f32_16x16x32_bf16 /
- * 32x32x16_bf16 vs v_mfma_f32_32x32x2_f32).  Replaces the same torchvision CNBlock Linears
- * and downsample convs as pipnet_linear_f32 / pipnet_conv2x2_f32.
- *   x: [B,H,W,Cin3] split planes (Cin3 = 3 Cin, % 32 == 0), w_packed: [Cout][Kp] bf16 with
- *   taps [KH][KW][Cin3] (Kp = KH*KW*Cin3 rounded up to 64, zero beyond), bias / scale [Cout]
- *   fp32 or NULL.  epilogue PIPNET_EPI_S3_GELU: y = split planes [B,OH,OW,3 Cout] bf16 of
+ * whose A rows are read as [hi(x) | lo(x) | hi(x)] and whose weight rows are
+ * [hi(w) | hi(w) | lo(w)] per tap.  Activations are stored as "split planes" [hi | lo]
+ * (2 Cin bf16 per pixel = the fp32 bytes); the kernel reads the third K segment from the
+ * hi plane again.  Per-product error ~1e-5 relative (fp32: 6e-8) at 3/16 of the fp32-MFMA
+ * cost (v_mfma_f32_16x16x32_bf16 / 32x32x16_bf16 vs v_mfma_f32_32x32x2_f32).  Replaces the
+ * same torchvision CNBlock Linears and downsample convs as pipnet_linear_f32 /
+ * pipnet_conv2x2_f32.
+ *   x: [B,H,W,2 Cin] split planes (Cin % 32 == 0), w_packed: [Cout][Kp] bf16 with taps
+ *   [KH][KW][3 Cin] (Kp = KH*KW*3Cin rounded up to 32, zero beyond), bias / scale [Cout]
+ *   fp32 or NULL.  epilogue PIPNET_EPI_S3_GELU: y = split planes [B,OH,OW,2 Cout] bf16 of
  *   gelu(conv + bias); PIPNET_EPI_F32_BIAS: y fp32 [B,OH,OW,Cout]; PIPNET_EPI_F32_RESID:
  *   y = R + scale * (conv + bias), fp32, R [B,OH,OW,Cout] (may equal y).  tile as
  *   pipnet_conv2d_nhwc_bf16_tile (only -1, 0, 4, 5). */
-int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin3, const void* w_packed,
+int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin, const void* w_packed,
                           const float* bias, const float* scale, const float* R, int Cout, int KH, int KW,
                           int stride, int pad, int epilogue, void* y, int tile, void* stream);
 
-/* pipnet_dwconv7_ln_f32 writing its output as split planes [B,H,W,3C] bf16 (the A operand of
- * the split-bf16 Linear1). */
+/* pipnet_dwconv7_ln_f32 writing its output as split planes [B,H,W,2C] bf16 [hi | lo] (the A
+ * operand of the split-bf16 Linear1). */
 int pipnet_dwconv7_ln_s3(const float* x, int B, int H, int W, int C, const float* w_packed,
                          const float* bias, const float* ln_w, const float* ln_b, void* y, void* stream);
 
-/* pipnet_layernorm_f32 writing split planes [rows, 3C] bf16 (input of a split-bf16 downsample conv). */
+/* pipnet_layernorm_f32 writing split planes [rows, 2C] bf16 (input of a split-bf16 downsample conv). */
 int pipnet_layernorm_s3(const float* x, int64_t rows, int C, const float* w, const float* b, void* y,
                         void* stream);
 
