@@ -14,7 +14,7 @@ constexpr int DW_THREADS = 192;
 // mean / variance, coalesced NHWC stores).  1-D grid, XCD-contiguous, so the halo rows of
 // neighbouring workgroups are served from one L2.  S3: the output is written as split-bf16
 // planes [hi | lo] (2C bf16 per pixel, the A operand of the split-bf16 Linear1).
-template <int C, int TX, int TY, int MINB, bool S3 = false>
+template <int C, int TX, int TY, int MINB, bool S3 = false, int LPP = 64>
 __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
                                                                       const float* __restrict__ wp,
                                                                       const float* __restrict__ bias,
@@ -24,7 +24,6 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
   constexpr int QC = C / 4;
   constexpr int G = DW_THREADS / QC;
   constexpr int NP = G * TX;
-  constexpr int NJ = (C + 63) / 64;
   __shared__ __attribute__((aligned(16))) float tile[TY * NP * C];
 
   const int tid = threadIdx.x;
@@ -74,34 +73,46 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
     for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
   __syncthreads();
 
+  // LayerNorm: LPP lanes per pixel (64 / LPP pixels per wave at once, log2(LPP)-step
+  // shuffle reductions -- one pixel per wave (LPP = 64) serialised two 6-step reductions
+  // per pixel); two-pass mean / variance as torch
+  constexpr int PPW = 64 / LPP;                 // pixels per wave per pass
+  constexpr int CJ = (C + LPP - 1) / LPP;       // channels per lane
   const int lane = tid & 63, wv = tid >> 6;
-  for (int pp = wv; pp < TY * NP; pp += DW_THREADS / 64) {
+  const int sub = lane / LPP, sl = lane % LPP;
+  for (int base = wv * PPW; base < TY * NP; base += (DW_THREADS / 64) * PPW) {
+    const int pp = base + sub;
     const int t = pp / NP, pix = pp - t * NP;
     const int ox = xblk + pix, oy = oy0 + t;
-    if (ox >= W || oy >= H) continue;
-    float vv[NJ];
+    const bool ok = pp < TY * NP && ox < W && oy < H;   // lane-group uniform; every lane shuffles
+    float vv[CJ];
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
-      vv[j] = (c < C) ? tile[pp * C + c] : 0.f;
+    for (int j = 0; j < CJ; ++j) {
+      const int c = sl + LPP * j;
+      vv[j] = (ok && c < C) ? tile[pp * C + c] : 0.f;
       s += vv[j];
     }
-    const float mean = wave_sum(s) * (1.0f / C);
+#pragma unroll
+    for (int o = LPP / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.0f / C);
     float qq = 0.f;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int c = lane + 64 * j;
+    for (int j = 0; j < CJ; ++j) {
+      const int c = sl + LPP * j;
       const float d = (c < C) ? vv[j] - mean : 0.f;
       qq = fmaf(d, d, qq);
     }
-    const float rstd = 1.0f / sqrtf(wave_sum(qq) * (1.0f / C) + LN_EPS);
+#pragma unroll
+    for (int o = LPP / 2; o > 0; o >>= 1) qq += __shfl_xor(qq, o, 64);
+    const float rstd = 1.0f / sqrtf(qq * (1.0f / C) + LN_EPS);
+    if (!ok) continue;
     const int64_t opix = ((int64_t)b * H + oy) * W + ox;
     if constexpr (S3) {
       __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 2 * C;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = lane + 64 * j;
+      for (int j = 0; j < CJ; ++j) {
+        const int c = sl + LPP * j;
         if (c < C) {
           __bf16 hi, lo;
           split_bf16((vv[j] - mean) * rstd * lnw[c] + lnb[c], hi, lo);
@@ -112,20 +123,20 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
     } else {
       float* dst = reinterpret_cast<float*>(yv) + opix * C;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int c = lane + 64 * j;
+      for (int j = 0; j < CJ; ++j) {
+        const int c = sl + LPP * j;
         if (c < C) dst[c] = (vv[j] - mean) * rstd * lnw[c] + lnb[c];
       }
     }
   }
 }
 
-template <int C, int TX, int TY, int MINB, bool S3 = false>
+template <int C, int TX, int TY, int MINB, bool S3 = false, int LPP = 64>
 inline int launch_dw(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
                      const float* lnb, void* y, hipStream_t s) {
   constexpr int NP = (DW_THREADS / (C / 4)) * TX;
   const dim3 grid(((W + NP - 1) / NP) * ((H + TY - 1) / TY) * B);
-  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX, TY, MINB, S3>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw,
+  hipLaunchKernelGGL((dwconv7_ln_kernel<C, TX, TY, MINB, S3, LPP>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp, bias, lnw,
                      lnb, y);
   return hipGetLastError() == hipSuccess ? PIPNET_OK : PIPNET_ERR_LAUNCH;
 }
