@@ -31,9 +31,15 @@ using CfgN64 = Cfg<4, 1, 2, 2, 32, 4>; // 256 x 64 (N = 64 layers), BK 32 x 4 st
 // Mirrored by kernels.py:bf16_conv_tile.
 // N >= 256 layers run the ping-pong 16x16x32 kernel (tile 5) at every batch size -- the
 // choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
-int conv_variant(int M, int N, bool pp_ok, bool s3 = false) {
+int conv_variant(int M, int N, bool pp_ok, bool s3 = false, int Kv = 0) {
+  if (s3) {  // split GEMMs (tools/s3_tiles.py, profiles/r01/s3_tiles.txt); tiles 0 / 4 / 5 / 7 only
+    const int m128 = ((M + 127) / 128) * ((N + 127) / 128) >= 512 ? 4 : 0;
+    if (!pp_ok) return m128;
+    if (N == 192) return 7;                          // one 192-wide tile instead of a 256-wide one
+    if (N == 384) return Kv >= 3 * 1024 ? 7 : m128;  // stage-3 Linear2: 192-wide; short K: 128x128
+    return N >= 256 ? 5 : m128;
+  }
   if (N >= 256 && pp_ok) return 5;
-  if (s3 && N >= 192 && pp_ok) return 5;   // split GEMMs: the ping-pong tile wins from N = 192 (tools/s3_tiles.py)
   if (N <= 64 && !s3) return 6;   // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
   const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
@@ -49,8 +55,28 @@ bool is_s3_epi(int epi) {
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
-  if (v < 0) v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi));
-  if (v > 6 || (v == 5 && !pp_ok)) return PIPNET_ERR_ARG;
+  if (v < 0) v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
+  if (v > 7 || ((v == 5 || v == 7) && !pp_ok)) return PIPNET_ERR_ARG;
+  if (v == 7) {                                  // 256 x 192 ping-pong (split epilogues only)
+    p.nt = (p.N + 191) / 192;
+    p.mt = (p.M + 255) / 256;
+    p.group_m = choose_group_m(p.K);
+    const dim3 grid(p.mt * p.nt);
+    switch (epi) {
+      case PIPNET_EPI_S3_GELU:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_S3_GELU, ALOAD, 3>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_F32_BIAS:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_F32_BIAS, ALOAD, 3>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_F32_RESID:
+        hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_F32_RESID, ALOAD, 3>), grid, dim3(512), 0, s, p);
+        break;
+      default: return PIPNET_ERR_ARG;
+    }
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   if (v == 5) {
     p.nt = (p.N + 255) / 256;
     p.mt = (p.M + 255) / 256;
@@ -254,7 +280,7 @@ extern "C" int pipnet_conv2d_nhwc_s3(const void* x, int B, int H, int W, int Cin
     return PIPNET_ERR_ARG;
   if (!is_s3_epi(epilogue)) return PIPNET_ERR_ARG;
   if (epilogue == PIPNET_EPI_F32_RESID && (!R || !scale)) return PIPNET_ERR_ARG;
-  if (tile != -1 && tile != 0 && tile != 4 && tile != 5) return PIPNET_ERR_ARG;
+  if (tile != -1 && tile != 0 && tile != 4 && tile != 5 && tile != 7) return PIPNET_ERR_ARG;
   if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
   if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y) || (R && !aligned16(R)) || (bias && !aligned16(bias)) ||
       (scale && !aligned16(scale)))

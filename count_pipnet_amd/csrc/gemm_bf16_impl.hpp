@@ -434,7 +434,11 @@ PIPNET_DEV void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int EPI, int ALOAD>
+// NB = B fragments (16 columns each) per wave: 4 -> 256-wide tiles, 3 -> 192-wide (N = 384 /
+// 192 layers: two 192-wide tiles instead of a full and a half-empty 256-wide one).  The DMA
+// and LDS layout stay those of the 256-wide tile (rows 192..255 are fetched and unused), so
+// the vmcnt accounting is identical.
+template <int EPI, int ALOAD, int NB = 4>
 __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   using namespace pp;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
@@ -443,7 +447,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   const int wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   int m0, n0;
-  tile_coords(p, BM, BN, m0, n0);
+  static_assert(NB == 3 || NB == 4, "NB");
+  constexpr int WCOLS = 16 * NB;                               // output columns per wave
+  tile_coords(p, BM, 4 * WCOLS, m0, n0);
   const int nk = p.K / BK;
 
   // ---- DMA sources: pieces wid and wid + 8 of A and of B (16 rows x 64 B each) ----
@@ -504,15 +510,15 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   };
   auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 64 + n * 16) * ROWB + fofs);
+    for (int n = 0; n < NB; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * WCOLS + n * 16) * ROWB + fofs);
   };
 
-  f32x4v acc[8][4];
+  f32x4v acc[8][NB];
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   // prologue: A(0) B(0) A(1) B(1) A(2) in flight (B(kt+2) is fetched in phase 0 of K-tile
   // kt, A(kt+3) in phase 1: two pieces per phase), wait for tile 0
@@ -537,7 +543,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+      for (int n = 0; n < NB; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     pp_barrier();
     // ---- phase 1: rows 64..127; fetch A of K-tile kt+3 (DMA first: an M0 write for the DMA
@@ -553,7 +559,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
+      for (int n = 0; n < NB; ++n)
         acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     pp_barrier();
@@ -566,8 +572,8 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
   float* wt = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
   const int c8 = lane & 7;
-  const int n = n0 + wc * 64 + 8 * c8;
-  const bool nok = n < p.N;
+  const int n = n0 + wc * WCOLS + 8 * c8;
+  const bool nok = c8 < 2 * NB && n < p.N;
   f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, s0 = b0, s1 = b0;
   if (EPI != PIPNET_EPI_NONE && p.bias && nok) {
     b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int nn = 0; nn < 4; ++nn)
+      for (int nn = 0; nn < NB; ++nn)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           wt[(r * 16 + 4 * (lane >> 4) + i) * EPI_LD + nn * 16 + fr] = acc[half * 4 + r][nn][i];

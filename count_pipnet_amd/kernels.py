@@ -187,12 +187,21 @@ def _chk_bf(t: Tensor, what: str) -> None:
         raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
 
 
-def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False) -> int:
+def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int = 0) -> int:
     """Workgroup tile the library picks (mirrors conv_variant in csrc/conv_bf16.hip):
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
     MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
-    if (n >= 256 or (s3 and n >= 192)) and pp_ok:
+    if s3:
+        m128 = 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
+        if not pp_ok:
+            return m128
+        if n == 192:
+            return 7
+        if n == 384:
+            return 7 if kv >= 3 * 1024 else m128
+        return 5 if n >= 256 else m128
+    if n >= 256 and pp_ok:
         return 5
     if n <= 64 and not s3:
         return 6
@@ -207,11 +216,13 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
 
 
 def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True,
-                          s3: bool = False) -> str:
+                          s3: bool = False, kv: int = 0) -> str:
     """rocprof name of the bf16 conv instantiation."""
-    t = bf16_conv_tile(m, n, pp_ok, s3) if tile < 0 else tile
+    t = bf16_conv_tile(m, n, pp_ok, s3, kv) if tile < 0 else tile
     if t == 5:
-        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}>"
+        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4>"
+    if t == 7:
+        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 3>"
     cfg, minb = _BF16_CFG[t]
     return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}>"
 
@@ -372,7 +383,7 @@ def conv_s3(x2: Tensor, w_packed: Tensor, kh: int, kw: int, cout: int, bias: Opt
         raise RuntimeError(f"conv_s3: out {tuple(out.shape)} {out.dtype} does not match {shape} {dt}")
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, True, s3=True), 2.0 * m * cout * k / 3.0,
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, True, s3=True, kv=k), 2.0 * m * cout * k / 3.0,
             lambda: _lib.call("pipnet_conv2d_nhwc_s3", x2.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
                               _ptr(scale), _ptr(r), cout, kh, kw, stride, pad, epilogue, out.data_ptr(), tile,
                               _stream(x2)))

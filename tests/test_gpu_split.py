@@ -41,7 +41,8 @@ def _gelu64(x):
 @pytest.mark.parametrize("b,h,cin,cout,kh,stride,tile", [
     (2, 13, 96, 384, 1, 1, -1), (3, 9, 96, 96, 1, 1, -1), (2, 11, 192, 192, 1, 1, 4), (2, 11, 192, 192, 1, 1, 0),
     (1, 7, 384, 1536, 1, 1, 5), (2, 7, 768, 256, 1, 1, -1), (4, 28, 96, 192, 2, 2, -1), (2, 27, 192, 384, 2, 1, -1),
-    (2, 13, 384, 768, 2, 1, 5), (3, 10, 128, 136, 1, 1, -1)])
+    (2, 13, 384, 768, 2, 1, 5), (3, 10, 128, 136, 1, 1, -1), (2, 13, 384, 384, 1, 1, 7), (1, 11, 192, 192, 1, 1, 7),
+    (2, 27, 192, 384, 2, 1, 7), (2, 9, 96, 200, 1, 1, 7)])
 @pytest.mark.parametrize("epi", ["f32_bias", "f32_resid", "s3_gelu"])
 def test_conv_s3_matches_split_product(gpu, b, h, cin, cout, kh, stride, tile, epi):
     g = torch.Generator().manual_seed(b * 1000 + h * 10 + kh)

@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--tiles", default="-1,0,4,5")
+    ap.add_argument("--tiles", default="-1,4,5,7")
     a = ap.parse_args()
     build.build()
     dev = torch.device("cuda:0")
