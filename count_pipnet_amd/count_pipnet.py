@@ -189,7 +189,8 @@ def detect_output_channels(features: nn.Module) -> int:
 
 def get_count_network(num_classes: int, args: argparse.Namespace, max_count: int = 3, use_ste: bool = True,
                       device=None):
-    """count_pipnet.py:324-436 -> (CountPIPNet, num_prototypes)."""
+    """count_pipnet.py:324-436 -> (CountPIPNet, num_prototypes).  Optional ``args.hip_dtype``
+    ("fp32" | "bf16x3") selects the HIP compute dtype of the ConvNeXt backbone."""
     if args.net not in base_architecture_to_features:
         raise ValueError(f"Network '{args.net}' is not supported. "
                          f"Supported networks: {list(base_architecture_to_features)}")
@@ -230,4 +231,7 @@ def get_count_network(num_classes: int, args: argparse.Namespace, max_count: int
     model = CountPIPNet(num_classes=num_classes, num_prototypes=num_prototypes, feature_net=features, args=args,
                         add_on_layers=add_on, classification_layer=classification, intermediate_layer=inter,
                         max_count=max_count, use_ste=use_ste, backward_clamp_strategy=backward_clamp_strategy)
+    if getattr(args, "hip_dtype", None):          # optional HIP compute dtype (pipnet.set_hip_dtype)
+        from .pipnet import set_hip_dtype
+        set_hip_dtype(model, args.hip_dtype)
     return model, num_prototypes

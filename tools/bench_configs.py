@@ -4,6 +4,7 @@
   C3  PIP-Net ResNet50 224x224, bs=128, bf16 (BASELINE C3) and fp32 (exact reference arithmetic)
   C5  CountPIPNet bilinear 2048 prototypes, 128x128, 64 images per GPU (bs=256 over 4 GPUs)
   C2' PIP-Net ConvNeXt-tiny-13 224x224, bs=64          (the 13x13 variant)
+  *_bf16x3: the same ConvNeXt configs with split-bf16 GEMMs (set_hip_dtype "bf16x3")
 
     python tools/bench_configs.py [--steps 10] [--only c5]
 Prints one JSON line per config (images/sec, ms/step, model TFLOP/s where defined).
@@ -40,6 +41,9 @@ CONFIGS = {
     "c2_13": dict(model="pipnet", batch=64, size=224, classes=200,
                   args=dict(net="convnext_tiny_13", num_features=0, bias=False), gflop=12.617),
 }
+# the split-bf16 build of every ConvNeXt config (fp32 in / out, three bf16 products per fp32 product)
+for _k in ("c1", "c5", "c2_13"):
+    CONFIGS[_k + "_bf16x3"] = dict(CONFIGS[_k], args=dict(CONFIGS[_k]["args"], hip_dtype="bf16x3"))
 
 
 def make(cfg, dev):
@@ -78,7 +82,7 @@ def main():
             el = time.perf_counter() - t0
         ips = cfg["batch"] * a.steps / el
         dt = cfg["args"].get("hip_dtype", "f32")
-        peak = 2500.0 if dt == "bf16" else 157.3
+        peak = 2500.0 if dt == "bf16" else 157.3      # bf16x3: fp32-equivalent TF/s against the fp32 peak
         rec = dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
                    image_size=cfg["size"], dtype=dt, model_tflops=ips * cfg["gflop"] / 1e3,
                    model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak)
