@@ -257,19 +257,32 @@ PIPNET_DEV float exp1_from_bits(uint32_t w) {
 // (first index on ties), y_soft at the argmax = 1 / sum exp(z - max), one-hot written as
 // (1 - y_soft) + y_soft (F.gumbel_softmax(hard=True)'s straight-through value).
 // P % 4 == 0.
-template <int NJ>
+//
+// SOFT (train mode, F.gumbel_softmax(hard=False), count_pipnet_utils.py:34-35): proto =
+// softmax((x - log E) / tau) written for every channel, and the per-prototype spatial sums
+// (the raw counts, count_pipnet.py:88) reduced per workgroup in LDS, one float atomic per
+// (workgroup, channel) into `sums`.
+template <int NJ, bool SOFT = false>
 __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float* __restrict__ logits, int HW, int P,
                                                                     float inv_tau,
                                                                     const float* __restrict__ exp_noise,
                                                                     uint64_t seed, uint64_t offset,
                                                                     const uint64_t* __restrict__ seed_dev,
                                                                     float* __restrict__ proto,
-                                                                    int32_t* __restrict__ hist) {
+                                                                    int32_t* __restrict__ hist,
+                                                                    float* __restrict__ sums = nullptr) {
   constexpr int NJ4 = (NJ + 3) / 4;         // float4 channel chunks per lane (256 channels each)
   if (seed_dev) seed = *seed_dev;            // graph-replay form: the seed lives in device memory
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  float racc[SOFT ? NJ4 : 1][4];
+  if constexpr (SOFT) {
+#pragma unroll
+    for (int j = 0; j < NJ4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) racc[j][e] = 0.f;
+  }
   for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
     const int pix = pix0 + pi;
     if (pix >= HW) break;
@@ -313,7 +326,28 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
 #pragma unroll
     for (int j = 0; j < NJ4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) sum += (4 * lane + 256 * j < P) ? expf(z[j][e] - m) : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const float ez = (4 * lane + 256 * j < P) ? expf(z[j][e] - m) : 0.f;
+        if constexpr (SOFT) z[j][e] = ez;
+        sum += ez;
+      }
+    if constexpr (SOFT) {
+      const float inv = 1.0f / wave_sum(sum);
+#pragma unroll
+      for (int j = 0; j < NJ4; ++j) {
+        const int c = 4 * lane + 256 * j;
+        if (c < P) {
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = z[j][e] * inv;
+            racc[j][e] += o[e];
+          }
+          st4(proto + base + c, o);
+        }
+      }
+      continue;
+    }
     const float ysoft = 1.0f / wave_sum(sum);              // softmax value at the argmax
     const float hard = (1.0f - ysoft) + ysoft;             // y_hard - y_soft + y_soft
 #pragma unroll
@@ -327,6 +361,20 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
       }
     }
     if (lane == 0) atomicAdd(hist + (int64_t)b * P + mi, 1);
+  }
+  if constexpr (SOFT) {
+    __shared__ float red[HEAD_THREADS / 64][NJ4 * 256];
+#pragma unroll
+    for (int j = 0; j < NJ4; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) red[wv][4 * lane + 256 * j + e] = racc[j][e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
+      float r = red[0][c];
+#pragma unroll
+      for (int w = 1; w < HEAD_THREADS / 64; ++w) r += red[w][c];
+      atomicAdd(sums + (int64_t)b * P + c, r);
+    }
   }
 }
 
@@ -493,6 +541,29 @@ extern "C" int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int H
   hipLaunchKernelGGL(seed_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, seed_state);
   PIPNET_CHECK_LAUNCH();
   return count_gumbel_launch(logits, B, HW, P, tau, nullptr, 0, 0, seed_state + 1, proto, hist, stream);
+}
+
+// Train-mode (soft) Gumbel head: proto = softmax((x - log E) / tau) [B,HW,P], sums [B,P] = spatial
+// sums (the raw counts; zeroed here).  exp_noise as pipnet_count_gumbel_f32 (NCHW) or NULL (Philox).
+extern "C" int pipnet_count_gumbel_soft_f32(const float* logits, int B, int HW, int P, float tau,
+                                            const float* exp_noise, uint64_t seed, uint64_t offset, float* proto,
+                                            float* sums, void* stream) {
+  if (B < 0 || HW <= 0 || P <= 0 || (P & 3) || !(tau > 0.f) || !logits || !proto || !sums) return PIPNET_ERR_ARG;
+  if (!aligned16(logits) || !aligned16(proto)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  const int nj = nj_bucket(P);
+  if (nj < 0) return PIPNET_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (!zero_fill(reinterpret_cast<uint32_t*>(sums), (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
+  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const float inv_tau = 1.0f / tau;
+#define CG_CALL(N)                                                                                                \
+  hipLaunchKernelGGL((count_gumbel_kernel<N, true>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau,      \
+                     exp_noise, seed, offset, nullptr, proto, nullptr, sums);
+  PIPNET_NJ_SWITCH(nj, CG_CALL)
+#undef CG_CALL
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
 }
 
 extern "C" int pipnet_count_finish_f32(const int32_t* hist, const float* sums, int B, int P, int max_count,

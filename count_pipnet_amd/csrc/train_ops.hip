@@ -194,6 +194,32 @@ __global__ __launch_bounds__(BWD_T) void nonneg_linear_bwd_kernel(const float* _
   }
 }
 
+// NonNegLinear input gradient: dx[r,p] = sum_k d_out[r,k] relu(W[k,p]) (the CountPIPNet finetune
+// phase back-propagates into a trainable intermediate layer).  One thread per (r, p), K small.
+__global__ __launch_bounds__(BWD_T) void nonneg_linear_dx_kernel(const float* __restrict__ d_out,
+                                                                 const float* __restrict__ W, int N, int D, int K,
+                                                                 float* __restrict__ dx) {
+  const int p = blockIdx.x * BWD_T + threadIdx.x;
+  const int r = blockIdx.y;
+  if (p >= D) return;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) acc = fmaf(d_out[(int64_t)r * K + k], fmaxf(W[(int64_t)k * D + p], 0.f), acc);
+  dx[(int64_t)r * D + p] = acc;
+}
+
+// BilinearIntermediate backward front (count_pipnet_utils.py:381-385, out = u * v with u = W(e),
+// v = V(e)): du = g * v, dv = g * u.
+__global__ __launch_bounds__(256) void bilinear_bwd_prep_kernel(const float* __restrict__ g,
+                                                                const float* __restrict__ u,
+                                                                const float* __restrict__ v, int64_t n,
+                                                                float* __restrict__ du, float* __restrict__ dv) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i];
+    du[i] = gi * v[i];
+    dv[i] = gi * u[i];
+  }
+}
+
 // torch.optim.AdamW (decoupled weight decay, amsgrad off), one parameter tensor, in torch's
 // float arithmetic (the host turns the double hyper-parameters into the same float
 // constants torch's foreach kernels receive: 1 - lr*wd, 1 - beta1, beta2, 1 - beta2, ...):
@@ -286,6 +312,26 @@ extern "C" int pipnet_clamp_min_f32(float* x, int64_t n, float lo, void* stream)
   if (n < 0 || !x) return PIPNET_ERR_ARG;
   if (n == 0) return PIPNET_OK;
   hipLaunchKernelGGL(clamp_min_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, lo);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_nonneg_linear_dx_f32(const float* d_out, const float* W, int N, int D, int K, float* dx,
+                                           void* stream) {
+  if (N < 0 || D <= 0 || K <= 0 || N > 65535 || !d_out || !W || !dx) return PIPNET_ERR_ARG;
+  if (N == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(nonneg_linear_dx_kernel, dim3((unsigned)((D + BWD_T - 1) / BWD_T), (unsigned)N), dim3(BWD_T), 0,
+                     (hipStream_t)stream, d_out, W, N, D, K, dx);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_bilinear_bwd_prep_f32(const float* g, const float* u, const float* v, int64_t n, float* du,
+                                            float* dv, void* stream) {
+  if (n < 0 || !g || !u || !v || !du || !dv) return PIPNET_ERR_ARG;
+  if (n == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(bilinear_bwd_prep_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, g, u, v, n, du,
+                     dv);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

@@ -470,6 +470,48 @@ def count_gumbel(logits_nhwc: Tensor, tau: float, exp_noise_nchw: Optional[Tenso
     return proto, hist
 
 
+def count_gumbel_soft(logits_nhwc: Tensor, tau: float, exp_noise_nchw: Optional[Tensor], seed: int,
+                      offset: int = 0) -> Tuple[Tensor, Tensor]:
+    """Train-mode (soft) Gumbel-softmax map [B,h,w,P] + fp32 spatial sums (raw counts) [B,P]."""
+    _chk(logits_nhwc, "prototype logits")
+    b, h, w, p = logits_nhwc.shape
+    if exp_noise_nchw is not None:
+        _chk(exp_noise_nchw, "exp noise")
+        if tuple(exp_noise_nchw.shape) != (b, p, h, w):
+            raise RuntimeError(f"exp noise shape {tuple(exp_noise_nchw.shape)} != {(b, p, h, w)}")
+    proto = torch.empty_like(logits_nhwc)
+    sums = torch.empty((b, p), device=logits_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_count_gumbel_soft_f32", logits_nhwc.data_ptr(), b, h * w, p, float(tau), _ptr(exp_noise_nchw),
+              int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), proto.data_ptr(), sums.data_ptr(),
+              _stream(logits_nhwc))
+    return proto, sums
+
+
+def nonneg_linear_dx(d_out: Tensor, w: Tensor) -> Tensor:
+    """d_out [N,K] relu(w [K,D]) -> [N,D] (NonNegLinear input gradient)."""
+    _chk(d_out, "d_out")
+    _chk(w, "classifier weight")
+    n, k = d_out.shape
+    if w.shape[0] != k:
+        raise RuntimeError(f"nonneg_linear_dx: d_out {tuple(d_out.shape)} vs W {tuple(w.shape)}")
+    dx = torch.empty((n, w.shape[1]), device=d_out.device, dtype=torch.float32)
+    _lib.call("pipnet_nonneg_linear_dx_f32", d_out.data_ptr(), w.data_ptr(), n, w.shape[1], k, dx.data_ptr(),
+              _stream(d_out))
+    return dx
+
+
+def bilinear_bwd_prep(g: Tensor, u: Tensor, v: Tensor) -> Tuple[Tensor, Tensor]:
+    """(g * v, g * u) for out = u * v."""
+    for t, what in ((g, "grad"), (u, "W(e)"), (v, "V(e)")):
+        _chk(t, what)
+    if not (g.shape == u.shape == v.shape):
+        raise RuntimeError("bilinear_bwd_prep: shape mismatch")
+    du, dv = torch.empty_like(g), torch.empty_like(g)
+    _lib.call("pipnet_bilinear_bwd_prep_f32", g.data_ptr(), u.data_ptr(), v.data_ptr(), g.numel(), du.data_ptr(),
+              dv.data_ptr(), _stream(g))
+    return du, dv
+
+
 def count_gumbel_devseed(logits_nhwc: Tensor, tau: float, seed_state: Tensor) -> Tuple[Tensor, Tensor]:
     """count_gumbel with the Philox key in device memory (seed_state: int64[2] on the device),
     advanced on the stream per call -- the form a captured HIP graph replays."""

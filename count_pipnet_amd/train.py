@@ -156,6 +156,135 @@ def hip_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor,
 
 
 # ------------------------------------------------------------------------------------------
+# CountPIPNet finetune phase (main.py:333-343): classifier + intermediate layer train
+# ------------------------------------------------------------------------------------------
+def hip_count_finetune_supported(net: nn.Module) -> bool:
+    """A ConvNeXt CountPIPNet (fp32, ROCm) whose trainable parameters are within the
+    classifier and an intermediate layer with a HIP backward (identity, one-hot, linear_full,
+    bilinear)."""
+    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    m = _inner(net)
+    if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+        return False
+    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, BilinearIntermediate)):
+        return False
+    if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
+        return False
+    allowed = {id(p) for p in m._classification.parameters()} | {id(p) for p in m._intermediate.parameters()}
+    return {id(p) for p in m.parameters() if p.requires_grad} <= allowed
+
+
+def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor]):
+    """CountPIPNet.forward(xs) in train mode (count_pipnet.py:70-110) on the HIP kernels, keeping
+    what the classifier / intermediate backward needs: (proto NHWC, raw counts, clamped
+    counts, intermediate activations dict, classifier input, out)."""
+    from . import _lib
+    from .count_pipnet_utils import BilinearIntermediate, GumbelSoftmax, LinearFull, OneHotEncoder
+    from .pipnet import add_on_logits_hip
+    feats = convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+    act = list(m._add_on)[-1] if isinstance(m._add_on, nn.Sequential) else m._add_on
+    if isinstance(act, GumbelSoftmax):
+        logits = add_on_logits_hip(m._add_on, feats, activation=GumbelSoftmax)
+        noise = act.exp_noise
+        if noise is not None:
+            proto, sums = K.count_gumbel_soft(logits, act.tau, noise.to(device=logits.device,
+                                                                        dtype=torch.float32).contiguous(), 0)
+        else:
+            seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())   # fresh noise per call
+            proto, sums = K.count_gumbel_soft(logits, act.tau, None, seed)
+    else:
+        logits = add_on_logits_hip(m._add_on, feats, activation=nn.Softmax)
+        proto, sums = K.softmax_pool(logits, pool_mode=1)
+    # train mode: STE round in the forward only with use_ste (count_pipnet.py:90-97)
+    counts, clamped = K.count_finish(None, sums, m._max_count, bool(m._use_ste))
+    layer = m._intermediate
+    saved = {}
+    if isinstance(layer, BilinearIntermediate):
+        e = K.linear(clamped, layer.embed.weight)
+        u = K.linear(e, layer.W.weight)
+        v = K.linear(e, layer.V.weight)
+        inter = torch.empty_like(u)
+        K.linear(e, layer.V.weight, epilogue=_lib.EPI_MUL, r=u, out=inter)
+        saved.update(e=e, u=u, v=v)
+    else:
+        from .count_pipnet import intermediate_hip
+        inter = intermediate_hip(layer, clamped)
+    _, out = K.nonneg_linear(inter, m._classification.weight, m._classification.bias, None)
+    return proto, counts, clamped, saved, inter, out
+
+
+def _intermediate_backward(layer: nn.Module, x: Tensor, saved: dict, d_inter: Tensor) -> None:
+    """Parameter gradients of the intermediate layer (its input, the clamped counts, is a
+    constant in the finetune phase: nothing upstream trains)."""
+    from . import _lib
+    from .count_pipnet_utils import BilinearIntermediate, LinearFull
+    if isinstance(layer, LinearFull):
+        _set_grad(layer.linear.weight, K.wgrad(d_inter, x))
+        if layer.linear.bias is not None:
+            _set_grad(layer.linear.bias, K.colsum(d_inter))
+    elif isinstance(layer, BilinearIntermediate):
+        e, u, v = saved["e"], saved["u"], saved["v"]
+        du, dv = K.bilinear_bwd_prep(d_inter, u, v)
+        if layer.W.weight.requires_grad:
+            _set_grad(layer.W.weight, K.wgrad(du, e))
+        if layer.V.weight.requires_grad:
+            _set_grad(layer.V.weight, K.wgrad(dv, e))
+        if layer.embed.weight.requires_grad:
+            de = K.linear(du, layer.W.weight.detach().t().contiguous())
+            ones = torch.ones(de.shape[1], device=de.device)
+            K.linear(dv, layer.V.weight.detach().t().contiguous(), None, _lib.EPI_RESID, scale=ones, r=de, out=de)
+            _set_grad(layer.embed.weight, K.wgrad(de, x))
+
+
+def hip_count_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor,
+                            optimizer_classifier: torch.optim.Optimizer, enforce_weight_sparsity: bool = True,
+                            tanh_loss_coeff: float = 1.0, sd_keep: Optional[Dict[int, Tensor]] = None,
+                            generator: Optional[torch.Generator] = None) -> Tensor:
+    """One CountPIPNet finetune iteration (train.py:75-140 with finetune=True,
+    is_count_pipnet=True): train-mode forward (soft Gumbel head, stochastic depth), the loss
+    kernel (loss = 2 * class; align / tanh over C * raw counts for logging), backward into the
+    classifier and the intermediate layer, AdamW for every parameter the classifier optimizer
+    holds (intermediate included when ``train_intermediate`` put it there), the sparsity clamps.
+    Returns the loss-kernel stats without synchronising."""
+    m = _inner(net)
+    cls = m._classification
+    xs = torch.cat([xs1, xs2])
+    if sd_keep is None:
+        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+    w_align, w_tanh, w_class = FINETUNE_LOSS_WEIGHTS
+    with torch.no_grad():
+        proto, counts, clamped, saved, inter, out = _count_train_forward(m, xs, sd_keep)
+        stats, d_out = K.train_loss(proto, counts, out, ys, cls.normalization_multiplier, enforce_weight_sparsity,
+                                    tanh_loss_coeff, w_align, w_tanh, w_class, "finetune")
+        train_b = cls.bias is not None and cls.bias.requires_grad
+        dw, db = K.nonneg_linear_backward(d_out, inter, cls.weight, train_b)
+        if cls.weight.requires_grad:
+            cls.weight.grad = dw
+        if train_b:
+            cls.bias.grad = db
+        layer = m._intermediate
+        if any(p.requires_grad for p in layer.parameters()):
+            _intermediate_backward(layer, clamped, saved, K.nonneg_linear_dx(d_out, cls.weight.detach()))
+        stepped = set()
+        for g in optimizer_classifier.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                post = None
+                if enforce_weight_sparsity:
+                    post = (SPARSITY_DELTA, 0.0) if p is cls.weight else (0.0, 0.0) if p is cls.bias else None
+                if hip_adamw_step(optimizer_classifier, p, p.grad, post):
+                    stepped.add(id(p))
+        if enforce_weight_sparsity:          # the clamps of parameters the optimizer did not touch
+            if id(cls.weight) not in stepped:
+                K.weight_sparsify_(cls.weight.detach(), SPARSITY_DELTA)
+            if cls.bias is not None and id(cls.bias) not in stepped:
+                K.clamp_min_(cls.bias.detach(), 0.0)
+            K.clamp_min_(cls.normalization_multiplier.detach(), 1.0)
+    return stats
+
+
+# ------------------------------------------------------------------------------------------
 # Pretrain / joint phases: a trainable backbone suffix + add-on (+ classifier) on the HIP
 # kernels (main.py:238-256 pretrain, :377-390 "train + freeze params")
 # ------------------------------------------------------------------------------------------
@@ -437,9 +566,18 @@ def train_pipnet(net, train_loader, optimizer_net, optimizer_classifier, schedul
     (``hip_finetune_step``) and the pretrain / joint phases with a trainable backbone suffix
     (``hip_train_step``).  Anything else (CountPIPNet, ResNet, a trainable stem) raises --
     run the reference's own loop on these modules (torch autograd path)."""
-    if is_count_pipnet or (pretrain and finetune):
-        raise NotImplementedError("count_pipnet_amd.train_pipnet: CountPIPNet training runs on the torch path")
-    if finetune and hip_finetune_supported(net):
+    if pretrain and finetune:
+        raise NotImplementedError("count_pipnet_amd.train_pipnet: pretrain and finetune are exclusive")
+    if is_count_pipnet:
+        if not (finetune and hip_count_finetune_supported(net)):
+            raise NotImplementedError("count_pipnet_amd.train_pipnet: only the CountPIPNet finetune phase has a HIP "
+                                      "step; run the reference train_pipnet with these modules for the others")
+        weights = FINETUNE_LOSS_WEIGHTS
+
+        def step(a, b, labels):
+            return hip_count_finetune_step(net, a, b, labels, optimizer_classifier, enforce_weight_sparsity,
+                                           tanh_loss_coeff, generator=generator)
+    elif finetune and hip_finetune_supported(net):
         weights = FINETUNE_LOSS_WEIGHTS
 
         def step(a, b, labels):

@@ -125,6 +125,21 @@ int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, co
                                  const float* bias, int Cout, int KH, int KW, int stride, int pad,
                                  const void* R, int epilogue, void* y, int tile, void* stream);
 
+/* ---- CountPIPNet finetune phase (pipnet/train.py:75-140, main.py:333-343: classifier +
+ * intermediate layer train) ------------------------------------------------------------
+ * Train-mode (soft) Gumbel head, F.gumbel_softmax(hard=False) (count_pipnet_utils.py:34-35):
+ * proto = softmax((x - log E) / tau) [B,HW,P] NHWC, sums [B,P] = spatial sums = the raw
+ * counts (count_pipnet.py:88).  exp_noise / seed / offset as pipnet_count_gumbel_f32. */
+int pipnet_count_gumbel_soft_f32(const float* logits, int B, int HW, int P, float tau, const float* exp_noise,
+                                 uint64_t seed, uint64_t offset, float* proto, float* sums, void* stream);
+
+/* dx = d_out relu(W)  (NonNegLinear input gradient; d_out [N,K], W [K,D], dx [N,D]). */
+int pipnet_nonneg_linear_dx_f32(const float* d_out, const float* W, int N, int D, int K, float* dx, void* stream);
+
+/* BilinearIntermediate backward front: du = g * v, dv = g * u (n elements). */
+int pipnet_bilinear_bwd_prep_f32(const float* g, const float* u, const float* v, int64_t n, float* du, float* dv,
+                                 void* stream);
+
 /* ---- split-bf16 ("bf16x3") fp32 path of the ConvNeXt backbone -------------------------
  * An fp32 operand x is carried as two bf16 values, hi = RNE(x) and lo = RNE(x - hi)
  * (x = hi + lo to ~2^-17 relative).  A product x.w is then hi.hi + lo.hi + hi.lo (the

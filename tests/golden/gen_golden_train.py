@@ -53,6 +53,11 @@ TRAIN_CASES = {
     "train_joint_mid_addon": ("pipnet_mid_addon", 3, 3, 303, True, "joint"),
     "train_pretrain_mid_addon": ("pipnet_mid_addon", 2, 3, 304, True, "pretrain"),
     "train_joint_c2": ("c2_pipnet_convnext26", 2, 2, 305, False, "joint"),
+    # CountPIPNet finetune (main.py:333-343: classifier + intermediate train; train_intermediate
+    # puts the intermediate into the classifier optimizer, util/args.py:318-321); soft Gumbel
+    # noise injected as in gen_golden (synth_exponential, seeds noise_seed + k per forward)
+    "train_count_finetune_onehot": ("count_onehot", 3, 3, 306, True, "count_finetune"),
+    "train_count_finetune_bilinear": ("count_bilinear_small", 3, 2, 307, True, "count_finetune"),
 }
 LR, WD = 0.05, 0.01
 
@@ -83,16 +88,20 @@ def run(name):
     import pipnet.train as ref_train
     from util.args import get_optimizer_nn
     dp = nn.DataParallel(net)
+    count = phase == "count_finetune"
     args = argparse.Namespace(net=case["net"], use_mid_layers=case.get("use_mid_layers", False),
                               num_stages=case.get("num_stages", 2), bias=case["bias"], lr=LR, lr_net=5e-4,
-                              lr_block=5e-4, weight_decay=WD, optimizer="Adam", seed=1, train_intermediate=False)
+                              lr_block=5e-4, weight_decay=WD, optimizer="Adam", seed=1, train_intermediate=count)
     with contextlib.redirect_stdout(io.StringIO()):
         opt_net, opt_cls, to_freeze, to_train, backbone = get_optimizer_nn(dp, args)
     for p in net.parameters():                       # main.py:335-339 (finetune)
         p.requires_grad = False
     for p in net._classification.parameters():
         p.requires_grad = phase != "pretrain"
-    if phase != "finetune":                          # main.py:240-249 / 377-385
+    if count and getattr(net, "_intermediate", None) is not None:     # main.py:341-343
+        for p in net._intermediate.parameters():
+            p.requires_grad = True
+    if phase not in ("finetune", "count_finetune"):   # main.py:240-249 / 377-385
         for group in (to_train, to_freeze, list(net._add_on.parameters())):
             for p in group:
                 p.requires_grad = True
@@ -122,13 +131,14 @@ def run(name):
     ref_train.calculate_loss = rec_loss
     h = net.register_forward_hook(hook)
     try:
-        with injected_bernoulli(seed=5000 + seed) as drawn, contextlib.redirect_stdout(io.StringIO()), \
-                contextlib.redirect_stderr(io.StringIO()):
+        with injected_bernoulli(seed=5000 + seed) as drawn, G.injected_exponential(seed=7000 + seed) as noise, \
+                contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
             info = ref_train.train_pipnet(dp, batches, opt_net, opt_cls,
                                           sched_net, None if phase == "pretrain" else sched_cls, criterion,
                                           1, 2 if phase == "pretrain" else 1, torch.device("cpu"),
-                                          is_count_pipnet=False, pretrain=phase == "pretrain",
-                                          finetune=phase == "finetune", enforce_weight_sparsity=True)
+                                          is_count_pipnet=count, pretrain=phase == "pretrain",
+                                          finetune=phase in ("finetune", "count_finetune"),
+                                          enforce_weight_sparsity=True)
     finally:
         h.remove()
         ref_train.calculate_loss = orig_loss
@@ -151,7 +161,10 @@ def run(name):
                 rec[f"s{i}_{k}"] = s[k].numpy()
         if keep_proto:
             rec[f"s{i}_w"] = s["w"].numpy()
-    if phase != "finetune":      # every trainable backbone / add-on tensor: full when small, else checksums
+    if count:                    # the trained intermediate tensors, in full (small cases)
+        for pname, prm in net._intermediate.named_parameters():
+            rec[f"inter/{pname}"] = prm.detach().numpy()
+    if phase not in ("finetune", "count_finetune"):   # every trainable backbone / add-on tensor
         for pname, prm in net.named_parameters():
             if prm.requires_grad and not pname.startswith("_classification"):
                 a = prm.detach().double()
@@ -175,6 +188,7 @@ def run(name):
     meta = dict(name=name, forward_case=fwd_case, phase=phase, iterations=nb, batch_per_view=bs, seed=seed,
                 lr_net=5e-4, lr_block=5e-4,
                 mask_seed=5000 + seed, masks_per_step=nmask, lr=LR, weight_decay=WD,
+                noise_seed=7000 + seed, noise_draws=len(noise),
                 steps=float(st["step"]), components=comps,
                 info={k: (v if isinstance(v, list) else float(v)) for k, v in info.items()},
                 torch=torch.__version__)
@@ -184,7 +198,10 @@ def run(name):
 
 def main():
     torch.set_num_threads(os.cpu_count() or 8)
+    only = sys.argv[1:]
     for name in TRAIN_CASES:
+        if only and name not in only:
+            continue
         rec = run(name)
         path = os.path.join(HERE, f"{name}.npz")
         np.savez_compressed(path, **rec)

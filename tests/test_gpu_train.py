@@ -26,7 +26,8 @@ from oracle import ref_cpu, train_ref
 
 pytestmark = pytest.mark.gpu
 NAMES = [n for n in train_golden_names() if n.startswith("train_finetune_")]
-SUFFIX = [n for n in train_golden_names() if not n.startswith("train_finetune_")]
+SUFFIX = [n for n in train_golden_names() if not n.startswith(("train_finetune_", "train_count_"))]
+COUNT = [n for n in train_golden_names() if n.startswith("train_count_finetune_")]
 
 
 def _t(a):
@@ -377,3 +378,83 @@ def test_suffix_gradients_match_autograd(gpu, name):
         scale = b.abs().max().item() + 1e-12
         err = (a - b).abs().max().item() / scale
         assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"
+
+
+# ---- CountPIPNet finetune phase: classifier + intermediate layer (main.py:333-343) -----------
+def _count_setup(name, gpu):
+    """The reference run's setup: finetune freeze (classifier + intermediate train), the
+    classifier optimizer of util/args.py:get_optimizer_nn with train_intermediate=True
+    (restated for the test), CosineAnnealingWarmRestarts as main.py:314."""
+    meta, rec, fwd_meta = load_train_golden(name)
+    net = build_model(fwd_meta).to(gpu).train()
+    cls = net._classification
+    for prm in net.parameters():
+        prm.requires_grad = False
+    for prm in list(cls.parameters()) + list(net._intermediate.parameters()):
+        prm.requires_grad = True
+    cls.normalization_multiplier.requires_grad = False
+    groups = [{"params": [cls.weight], "lr": meta["lr"], "weight_decay": meta["weight_decay"]},
+              {"params": [] if cls.bias is None else [cls.bias], "lr": meta["lr"], "weight_decay": 0.0},
+              {"params": list(net._intermediate.parameters()), "lr": meta["lr"],
+               "weight_decay": meta["weight_decay"]}]
+    opt = torch.optim.AdamW(groups, lr=meta["lr"], weight_decay=0.0)
+    sched = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt, T_0=10, eta_min=0.001, T_mult=1)
+    c = fwd_meta["case"]
+    batches = train_loader_batches(c["size"], c["num_classes"], meta["iterations"], meta["batch_per_view"],
+                                   meta["seed"])
+    return meta, rec, fwd_meta, net, opt, sched, batches
+
+
+@pytest.mark.parametrize("name", COUNT)
+def test_count_finetune_iterations_match_reference(gpu, name):
+    """The reference's own train_pipnet(finetune=True, is_count_pipnet=True) run, replayed on
+    the HIP step with its stochastic-depth masks and Gumbel noise: soft Gumbel map, raw counts
+    and logits of every forward, the loss terms, and the classifier / intermediate tensors
+    after the run (99 % / 95 % elementwise quorum: AdamW's first steps move each weight by
+    ~lr * sign(grad), so a gradient near 0 may take either sign)."""
+    from count_pipnet_amd.synthetic import synth_exponential
+    meta, rec, fwd_meta, net, opt, sched, batches = _count_setup(name, gpu)
+    assert T.hip_count_finetune_supported(net)
+    act = list(net._add_on)[-1]
+    iters = len(batches)
+    for i, (xs1, xs2, ys) in enumerate(batches):
+        sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
+        act.exp_noise = synth_exponential(tuple(rec[f"s{i}_proto"].shape), meta["noise_seed"] + i).to(gpu)
+        with torch.no_grad():
+            proto, counts, clamped, _, _, out = T._count_train_forward(net, torch.cat([xs1, xs2]).to(gpu), sd_keep)
+        torch.testing.assert_close(proto.permute(0, 3, 1, 2).cpu(), _t(rec[f"s{i}_proto"]), rtol=1e-3, atol=1e-4)
+        r_counts = _t(rec[f"s{i}_pooled"])
+        torch.testing.assert_close(counts.cpu(), r_counts, rtol=1e-4, atol=1e-3)
+        # rows whose soft count sits on a rounding boundary may round the other way
+        ok = ((r_counts - r_counts.floor() - 0.5).abs() > 1e-3).all(dim=1)
+        torch.testing.assert_close(out.cpu()[ok], _t(rec[f"s{i}_out"])[ok], rtol=1e-3, atol=2e-3)
+        opt.zero_grad(set_to_none=True)
+        stats = T.hip_count_finetune_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt, True, 1.0,
+                                          sd_keep=sd_keep).cpu()
+        comp = meta["components"][i]
+        assert float(stats[2]) == pytest.approx(comp["class"], rel=1e-3, abs=1e-4)
+        assert float(stats[1]) == pytest.approx(comp["tanh"], rel=1e-3, abs=1e-4)
+        assert float(stats[0]) == pytest.approx(comp["align"], rel=1e-3, abs=1e-4)
+        assert float(stats[3]) == pytest.approx(comp["loss"], rel=1e-3, abs=1e-4)
+        sched.step(0 + i / iters)
+    bound = 4 * meta["lr"] * iters + 1e-6
+    cls = net._classification
+    _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, max_abs=bound)
+    _quorum_close(opt.state[cls.weight]["exp_avg"], _t(rec["final_w_exp_avg"]), 1e-3, 1e-7)
+    assert float(cls.normalization_multiplier[0]) == pytest.approx(float(rec["final_mult"][0]))
+    inter = dict(net._intermediate.named_parameters())
+    keys = [k for k in rec if k.startswith("inter/")]
+    assert sorted(k[6:] for k in keys) == sorted(inter)
+    for k in keys:
+        _quorum_close(inter[k[6:]], _t(rec[k]), 1e-4, 1e-5, frac=0.95, max_abs=bound)
+
+
+def test_count_train_pipnet_epoch(gpu):
+    """count_pipnet_amd.train_pipnet(is_count_pipnet=True, finetune=True) drives the HIP step."""
+    name = COUNT[0]
+    meta, rec, fwd_meta, net, opt, sched, batches = _count_setup(name, gpu)
+    with contextlib.redirect_stdout(io.StringIO()):
+        info = T.train_pipnet(net, batches, opt, opt, None, sched, None, 1, 1, gpu, is_count_pipnet=True,
+                              finetune=True)
+    assert len(info["lrs_class"]) == len(batches)
+    assert np.isfinite(info["loss"]) and info["loss"] > 0

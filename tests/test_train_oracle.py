@@ -25,7 +25,8 @@ FINETUNE = [n for n in NAMES if n.startswith("train_finetune_")]
 
 def _loss_weights(meta):
     """(align, tanh, class) weights of train.py:51-61 for the fixture's phase (epoch 1)."""
-    return {"pretrain": (0.5, 5.0, 0.0), "joint": (5.0, 2.0, 2.0), "finetune": (0.0, 0.0, 2.0)}[meta["phase"]]
+    return {"pretrain": (0.5, 5.0, 0.0), "joint": (5.0, 2.0, 2.0), "finetune": (0.0, 0.0, 2.0),
+            "count_finetune": (0.0, 0.0, 2.0)}[meta["phase"]]
 
 
 def _t(a):
