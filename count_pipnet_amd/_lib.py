@@ -37,6 +37,9 @@ SIGNATURES = {
     "pipnet_count_gumbel_soft_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_nonneg_linear_dx_f32": [P, P, I32, I32, I32, P, P],
     "pipnet_bilinear_bwd_prep_f32": [P, P, P, I64, P, P, P],
+    "pipnet_count_ste_bwd_f32": [P, I64, I32, I32, I32, P, P, P],
+    "pipnet_onehot_ste_bwd_f32": [P, I64, I32, P, I32, I32, P, P, P],
+    "pipnet_count_head_bwd_f32": [P, P, I32, I32, I32, P, F32, F32, F32, F32, P, P, P],
     "pipnet_conv2d_nhwc_s3": [P, I32, I32, I32, I32, P, P, P, P, I32, I32, I32, I32, I32, I32, P, I32, P],
     "pipnet_dwconv7_ln_s3": [P, I32, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_layernorm_s3": [P, I64, I32, P, P, P, P],

@@ -489,6 +489,7 @@ __global__ __launch_bounds__(256) void argmax_hw_kernel(const float* __restrict_
 __global__ __launch_bounds__(256) void pool_grad_kernel(const float* __restrict__ pooled, int Bh, int P,
                                                         const float* __restrict__ d_out, const float* __restrict__ W,
                                                         int K, float w_tanh, float coeff,
+                                                        const float* __restrict__ extra,
                                                         float* __restrict__ dpool) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int N = 2 * Bh;
@@ -505,16 +506,20 @@ __global__ __launch_bounds__(256) void pool_grad_kernel(const float* __restrict_
     const float th = tanhf(s);
     g += -0.5f * w_tanh / (float)P * coeff * (1.f - th * th) / (th + 1e-8f);
   }
+  if (extra) g += extra[t];
   dpool[t] = g;
 }
 
 // One wave per pixel pair (view 1 pixel n, view 2 pixel n): align gradient, max-pool
 // scatter, softmax backward -> d logits.  a = align weight / 2 / (Bh*HW).
-template <int NJ4>
+// SUM (CountPIPNet, count_pipnet.py:88 counts = proto.sum((2,3))): every pixel receives
+// dpool[b,p]; the softmax backward is scaled by oscale = 1/tau (soft Gumbel-softmax,
+// y = softmax((x + g)/tau), the noise g a constant).
+template <int NJ4, bool SUM = false>
 __global__ __launch_bounds__(TB_T) void head_bwd_kernel(const float* __restrict__ proto, int Bh, int HW, int P,
                                                         const int32_t* __restrict__ amax,
                                                         const float* __restrict__ dpool, float a,
-                                                        float* __restrict__ dlogits) {
+                                                        float* __restrict__ dlogits, float oscale = 1.f) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t npix = (int64_t)Bh * HW;
   for (int64_t n = (int64_t)blockIdx.x * 4 + wv; n < npix; n += (int64_t)gridDim.x * 4) {
@@ -543,8 +548,8 @@ __global__ __launch_bounds__(TB_T) void head_bwd_kernel(const float* __restrict_
       if (c < P) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (amax[(int64_t)b1 * P + c + e] == hw) g1[j][e] += dpool[(int64_t)b1 * P + c + e];
-          if (amax[(int64_t)b2 * P + c + e] == hw) g2[j][e] += dpool[(int64_t)b2 * P + c + e];
+          if (SUM || amax[(int64_t)b1 * P + c + e] == hw) g1[j][e] += dpool[(int64_t)b1 * P + c + e];
+          if (SUM || amax[(int64_t)b2 * P + c + e] == hw) g2[j][e] += dpool[(int64_t)b2 * P + c + e];
           s1 = fmaf(g1[j][e], y1[j][e], s1);
           s2 = fmaf(g2[j][e], y2[j][e], s2);
         }
@@ -556,8 +561,8 @@ __global__ __launch_bounds__(TB_T) void head_bwd_kernel(const float* __restrict_
     for (int j = 0; j < NJ4; ++j) {
       const int c = 4 * lane + 256 * j;
       if (c < P) {
-        st4(dlogits + n * P + c, y1[j] * (g1[j] - s1));
-        st4(dlogits + (npix + n) * P + c, y2[j] * (g2[j] - s2));
+        st4(dlogits + n * P + c, y1[j] * (g1[j] - s1) * oscale);
+        st4(dlogits + (npix + n) * P + c, y2[j] * (g2[j] - s2) * oscale);
       }
     }
   }
@@ -695,7 +700,7 @@ extern "C" int pipnet_head_bwd_f32(const float* proto, const float* pooled, int 
                      argmax_ws);
   PIPNET_CHECK_LAUNCH();
   hipLaunchKernelGGL(pool_grad_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, pooled, Bh, P, d_out, W,
-                     K, w_tanh, tanh_coeff, dpool_ws);
+                     K, w_tanh, tanh_coeff, nullptr, dpool_ws);
   PIPNET_CHECK_LAUNCH();
   const float a = 0.5f * w_align / (float)((int64_t)Bh * HW);
 #define PIPNET_HB(NJ)                                                                                            \
@@ -703,6 +708,139 @@ extern "C" int pipnet_head_bwd_f32(const float* proto, const float* pooled, int 
                      a, d_logits);
   PIPNET_BY_NJ4(P, PIPNET_HB)
 #undef PIPNET_HB
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+// ---- CountPIPNet head / count backward (pretrain and joint phases) -------------------------
+// d counts of the STE chain (count_pipnet.py:90-97): counts_raw -> [STE_Round] -> ClampSTE(0,
+// max) -> intermediate.  STE_Round passes the gradient through (count_pipnet_utils.py:52-55);
+// ClampSTE "Gated" (:67-84) keeps it where its input lies in [0, max], "Identity" passes it.
+// Without STE the forward is torch.clamp(counts) (train mode: no rounding), whose backward is
+// the same gate on the raw counts.
+__global__ __launch_bounds__(256) void count_ste_bwd_kernel(const float* __restrict__ counts, int64_t n,
+                                                            float max_count, int use_ste, int gated,
+                                                            const float* __restrict__ d_clamped,
+                                                            float* __restrict__ d_counts) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float x = use_ste ? rintf(counts[i]) : counts[i];
+    const bool pass = !gated || (x >= 0.f && x <= max_count);
+    d_counts[i] = pass ? d_clamped[i] : 0.f;
+  }
+}
+
+// ModifiedSTEFunction.backward (count_pipnet_utils.py:226-321) over rows (b,p) of the
+// encoding gradient g [rows][M].  x = the encoder's input (clamped counts); r = rint(x);
+// cur = clamp(int(r) - 1, 0, M - 1).  Rows with r < 0.1 get 0 (the reference's chained
+// mask assignment `counts_grad[zero_mask][neg] = ...` writes a temporary).  Otherwise, with
+// (mn, mi) = min over M (first index) and allpos = mn > 0:
+//   strategy 2 ('max_grad') and some non-zero row of the batch allpos: allpos rows -> max
+//     over M; the others 0 (`final_grad_nz[std][dec] = ...` also writes a temporary);
+//   else: mag = |mn| (strategy 1 'current_grad' and allpos: g[cur]); mi < cur -> +mag,
+//     mi > cur -> -mag, else 0;
+//   respect_active and g[cur] < 0 -> 0.
+__device__ __forceinline__ void onehot_row(const float* __restrict__ g, int M, float& mn, int& mi, float& mx) {
+  mn = g[0]; mi = 0; mx = g[0];
+  for (int k = 1; k < M; ++k) {
+    const float v = g[k];
+    if (v < mn) { mn = v; mi = k; }
+    mx = fmaxf(mx, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void onehot_ste_flag_kernel(const float* __restrict__ x, int64_t rows, int M,
+                                                              const float* __restrict__ g, int* __restrict__ flag) {
+  bool any = false;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
+    if (!(rintf(x[i]) < 0.1f)) {
+      float mn, mx;
+      int mi;
+      onehot_row(g + i * M, M, mn, mi, mx);
+      any |= mn > 0.f;
+    }
+  }
+  if (__ballot(any) != 0 && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+__global__ void zero_flag_kernel(int* __restrict__ flag) {
+  if (threadIdx.x == 0) *flag = 0;
+}
+
+__global__ __launch_bounds__(256) void onehot_ste_bwd_kernel(const float* __restrict__ x, int64_t rows, int M,
+                                                             const float* __restrict__ g, int strategy,
+                                                             int respect_active, const int* __restrict__ flag,
+                                                             float* __restrict__ dx) {
+  const bool global_allpos = strategy == 2 && *flag;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < rows; i += (int64_t)gridDim.x * 256) {
+    const float r = rintf(x[i]);
+    float out = 0.f;
+    if (!(r < 0.1f)) {
+      const float* gi = g + i * M;
+      int cur = (int)r - 1;
+      cur = cur < 0 ? 0 : (cur > M - 1 ? M - 1 : cur);
+      float mn, mx;
+      int mi;
+      onehot_row(gi, M, mn, mi, mx);
+      const bool allpos = mn > 0.f;
+      if (global_allpos) {
+        out = allpos ? mx : 0.f;
+      } else {
+        const float mag = (strategy == 1 && allpos) ? gi[cur] : fabsf(mn);
+        out = mi < cur ? mag : (mi > cur ? -mag : 0.f);
+      }
+      if (respect_active && gi[cur] < 0.f) out = 0.f;
+    }
+    dx[i] = out;
+  }
+}
+
+extern "C" int pipnet_count_ste_bwd_f32(const float* counts, int64_t n, int max_count, int use_ste, int gated,
+                                        const float* d_clamped, float* d_counts, void* stream) {
+  if (n < 0 || max_count < 0 || !counts || !d_clamped || !d_counts) return PIPNET_ERR_ARG;
+  if (n == 0) return PIPNET_OK;
+  hipLaunchKernelGGL(count_ste_bwd_kernel, dim3(grid_cap(n)), dim3(256), 0, (hipStream_t)stream, counts, n,
+                     (float)max_count, use_ste, gated, d_clamped, d_counts);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_onehot_ste_bwd_f32(const float* x, int64_t rows, int M, const float* g, int strategy,
+                                         int respect_active, int* flag_ws, float* dx, void* stream) {
+  if (rows < 0 || M <= 0 || strategy < 0 || strategy > 2 || !x || !g || !flag_ws || !dx) return PIPNET_ERR_ARG;
+  if (rows == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(zero_flag_kernel, dim3(1), dim3(64), 0, s, flag_ws);
+  PIPNET_CHECK_LAUNCH();
+  if (strategy == 2) {
+    hipLaunchKernelGGL(onehot_ste_flag_kernel, dim3(grid_cap(rows)), dim3(256), 0, s, x, rows, M, g, flag_ws);
+    PIPNET_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(onehot_ste_bwd_kernel, dim3(grid_cap(rows)), dim3(256), 0, s, x, rows, M, g, strategy,
+                     respect_active, flag_ws, dx);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+// d logits of the CountPIPNet head: counts = spatial sums of proto = softmax((logits + g)/tau)
+// (tau = 1, g = 0 for the plain Softmax add-on).  d counts = d_counts_in (the classifier /
+// intermediate / STE chain, may be NULL) + the tanh term on C * counts; the align term as the
+// PIP-Net head.  proto NHWC [2Bh][HW][P], counts [2Bh][P], dcnt_ws float [2Bh*P].
+extern "C" int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, int HW, int P,
+                                         const float* d_counts_in, float w_align, float w_tanh, float tanh_coeff,
+                                         float inv_tau, float* dcnt_ws, float* d_logits, void* stream) {
+  if (Bh <= 0 || HW <= 0 || P <= 0 || (P & 3) || !proto || !counts || !dcnt_ws || !d_logits) return PIPNET_ERR_ARG;
+  if (!aligned16(proto) || !aligned16(d_logits)) return PIPNET_ERR_ALIGN;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t NP = (int64_t)2 * Bh * P;
+  hipLaunchKernelGGL(pool_grad_kernel, dim3((unsigned)((NP + 255) / 256)), dim3(256), 0, s, counts, Bh, P, nullptr,
+                     nullptr, 0, w_tanh, tanh_coeff, d_counts_in, dcnt_ws);
+  PIPNET_CHECK_LAUNCH();
+  const float a = 0.5f * w_align / (float)((int64_t)Bh * HW);
+#define PIPNET_CHB(NJ)                                                                                           \
+  hipLaunchKernelGGL((head_bwd_kernel<NJ, true>), dim3(TB_G * 2), dim3(TB_T), 0, s, proto, Bh, HW, P, nullptr,  \
+                     dcnt_ws, a, d_logits, inv_tau);
+  PIPNET_BY_NJ4(P, PIPNET_CHB)
+#undef PIPNET_CHB
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

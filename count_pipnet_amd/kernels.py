@@ -512,6 +512,60 @@ def bilinear_bwd_prep(g: Tensor, u: Tensor, v: Tensor) -> Tuple[Tensor, Tensor]:
     return du, dv
 
 
+ONEHOT_STRATEGY = {None: 0, "none": 0, "current_grad": 1, "max_grad": 2}
+
+
+def count_ste_backward(counts: Tensor, d_clamped: Tensor, max_count: int, use_ste: bool, gated: bool) -> Tensor:
+    """d raw counts from d clamped counts through STE_Round / ClampSTE (count_pipnet.py:90-97)."""
+    _chk(counts, "counts")
+    _chk(d_clamped, "d clamped counts")
+    if counts.shape != d_clamped.shape:
+        raise RuntimeError(f"count_ste_backward: counts {tuple(counts.shape)} vs grad {tuple(d_clamped.shape)}")
+    d = torch.empty_like(counts)
+    _lib.call("pipnet_count_ste_bwd_f32", counts.data_ptr(), counts.numel(), int(max_count), int(bool(use_ste)),
+              int(bool(gated)), d_clamped.data_ptr(), d.data_ptr(), _stream(counts))
+    return d
+
+
+def onehot_ste_backward(x: Tensor, g: Tensor, strategy: Optional[str] = None, respect_active: bool = False) -> Tensor:
+    """ModifiedSTEFunction.backward (count_pipnet_utils.py:226-321): x [B,P] encoder input,
+    g [B,P*M] (or [B,P,M]) encoding gradient -> d x [B,P]."""
+    _chk(x, "one-hot encoder input")
+    _chk(g, "encoding gradient")
+    b, p = x.shape
+    if g.numel() % max(x.numel(), 1) or g.shape[0] != b:
+        raise RuntimeError(f"onehot_ste_backward: x {tuple(x.shape)} vs grad {tuple(g.shape)}")
+    if strategy not in ONEHOT_STRATEGY:
+        raise ValueError(f"Unknown positive_grad_strategy {strategy!r}")
+    m = g.numel() // max(x.numel(), 1)
+    dx = torch.empty_like(x)
+    flag = torch.empty(1, device=x.device, dtype=torch.int32)
+    _lib.call("pipnet_onehot_ste_bwd_f32", x.data_ptr(), x.numel(), m, g.data_ptr(), ONEHOT_STRATEGY[strategy],
+              int(bool(respect_active)), flag.data_ptr(), dx.data_ptr(), _stream(x))
+    return dx
+
+
+def count_head_backward(proto_nhwc: Tensor, counts: Tensor, d_counts: Optional[Tensor], w_align: float,
+                        w_tanh: float, tanh_coeff: float, tau: float) -> Tensor:
+    """d loss / d logits of the CountPIPNet head (soft Gumbel-softmax / softmax, spatial sum)
+    for the align / tanh terms of calculate_loss plus the classifier chain's d counts."""
+    _chk(proto_nhwc, "proto features")
+    _chk(counts, "counts")
+    n, h, ww, p = proto_nhwc.shape
+    if tuple(counts.shape) != (n, p) or n % 2:
+        raise RuntimeError(f"count_head_backward: proto {tuple(proto_nhwc.shape)} vs counts {tuple(counts.shape)}")
+    if d_counts is not None:
+        _chk(d_counts, "d counts")
+        if d_counts.shape != counts.shape:
+            raise RuntimeError("count_head_backward: d counts shape")
+    d_logits = torch.empty_like(proto_nhwc)
+    dcnt = torch.empty((n, p), device=proto_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_count_head_bwd_f32", proto_nhwc.data_ptr(), counts.data_ptr(), n // 2, h * ww, p,
+              _ptr(d_counts), float(w_align), float(w_tanh), float(tanh_coeff), 1.0 / float(tau), dcnt.data_ptr(),
+              d_logits.data_ptr(), _stream(proto_nhwc))
+    return d_logits
+
+
 def count_gumbel_devseed(logits_nhwc: Tensor, tau: float, seed_state: Tensor) -> Tuple[Tensor, Tensor]:
     """count_gumbel with the Philox key in device memory (seed_state: int64[2] on the device),
     advanced on the stream per call -- the form a captured HIP graph replays."""

@@ -174,14 +174,21 @@ def hip_count_finetune_supported(net: nn.Module) -> bool:
     return {id(p) for p in m.parameters() if p.requires_grad} <= allowed
 
 
-def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor]):
+def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor], j: Optional[int] = None):
     """CountPIPNet.forward(xs) in train mode (count_pipnet.py:70-110) on the HIP kernels, keeping
-    what the classifier / intermediate backward needs: (proto NHWC, raw counts, clamped
-    counts, intermediate activations dict, classifier input, out)."""
+    what the backward needs: (proto NHWC, raw counts, clamped counts, intermediate activations
+    dict, classifier input, out).  With ``j`` the backbone suffix features[j:] runs with its
+    activations kept (``_forward_saving``); they and the features are added to the dict
+    (``feats``, ``suffix``) together with the head's temperature (``tau``)."""
     from . import _lib
-    from .count_pipnet_utils import BilinearIntermediate, GumbelSoftmax, LinearFull, OneHotEncoder
+    from .count_pipnet_utils import BilinearIntermediate, GumbelSoftmax
     from .pipnet import add_on_logits_hip
-    feats = convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+    saved = {}
+    if j is None:
+        feats = convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+    else:
+        feats, saved["suffix"] = _forward_saving(m, xs, j, sd_keep)
+        saved["feats"] = feats
     act = list(m._add_on)[-1] if isinstance(m._add_on, nn.Sequential) else m._add_on
     if isinstance(act, GumbelSoftmax):
         logits = add_on_logits_hip(m._add_on, feats, activation=GumbelSoftmax)
@@ -192,13 +199,15 @@ def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor]):
         else:
             seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())   # fresh noise per call
             proto, sums = K.count_gumbel_soft(logits, act.tau, None, seed)
+        saved["tau"] = float(act.tau)
     else:
         logits = add_on_logits_hip(m._add_on, feats, activation=nn.Softmax)
         proto, sums = K.softmax_pool(logits, pool_mode=1)
+        saved["tau"] = 1.0
+    del logits
     # train mode: STE round in the forward only with use_ste (count_pipnet.py:90-97)
     counts, clamped = K.count_finish(None, sums, m._max_count, bool(m._use_ste))
     layer = m._intermediate
-    saved = {}
     if isinstance(layer, BilinearIntermediate):
         e = K.linear(clamped, layer.embed.weight)
         u = K.linear(e, layer.W.weight)
@@ -213,27 +222,42 @@ def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor]):
     return proto, counts, clamped, saved, inter, out
 
 
-def _intermediate_backward(layer: nn.Module, x: Tensor, saved: dict, d_inter: Tensor) -> None:
-    """Parameter gradients of the intermediate layer (its input, the clamped counts, is a
-    constant in the finetune phase: nothing upstream trains)."""
+def _intermediate_backward(layer: nn.Module, x: Tensor, saved: dict, d_inter: Tensor,
+                           need_dx: bool = False) -> Optional[Tensor]:
+    """Parameter gradients of the intermediate layer (count_pipnet_utils.py:323-539) and, with
+    ``need_dx``, the gradient w.r.t. its input x (the clamped counts) -- None where no gradient
+    flows (a OneHotEncoder without STE: create_modified_encoding is not differentiable)."""
     from . import _lib
-    from .count_pipnet_utils import BilinearIntermediate, LinearFull
+    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    if isinstance(layer, IdentityIntermediate):
+        return d_inter if need_dx else None
+    if isinstance(layer, OneHotEncoder):
+        if not (need_dx and layer.use_ste):
+            return None
+        return K.onehot_ste_backward(x, d_inter, layer.positive_grad_strategy, layer.respect_active_grad)
     if isinstance(layer, LinearFull):
-        _set_grad(layer.linear.weight, K.wgrad(d_inter, x))
-        if layer.linear.bias is not None:
+        w = layer.linear.weight
+        if w.requires_grad:
+            _set_grad(w, K.wgrad(d_inter, x))
+        if layer.linear.bias is not None and layer.linear.bias.requires_grad:
             _set_grad(layer.linear.bias, K.colsum(d_inter))
-    elif isinstance(layer, BilinearIntermediate):
+        return K.linear(d_inter, w.detach().t().contiguous(), None, _lib.EPI_NONE) if need_dx else None
+    if isinstance(layer, BilinearIntermediate):
         e, u, v = saved["e"], saved["u"], saved["v"]
         du, dv = K.bilinear_bwd_prep(d_inter, u, v)
         if layer.W.weight.requires_grad:
             _set_grad(layer.W.weight, K.wgrad(du, e))
         if layer.V.weight.requires_grad:
             _set_grad(layer.V.weight, K.wgrad(dv, e))
+        if not (layer.embed.weight.requires_grad or need_dx):
+            return None
+        de = K.linear(du, layer.W.weight.detach().t().contiguous())
+        ones = torch.ones(de.shape[1], device=de.device)
+        K.linear(dv, layer.V.weight.detach().t().contiguous(), None, _lib.EPI_RESID, scale=ones, r=de, out=de)
         if layer.embed.weight.requires_grad:
-            de = K.linear(du, layer.W.weight.detach().t().contiguous())
-            ones = torch.ones(de.shape[1], device=de.device)
-            K.linear(dv, layer.V.weight.detach().t().contiguous(), None, _lib.EPI_RESID, scale=ones, r=de, out=de)
             _set_grad(layer.embed.weight, K.wgrad(de, x))
+        return K.linear(de, layer.embed.weight.detach().t().contiguous(), None, _lib.EPI_NONE) if need_dx else None
+    raise NotImplementedError(f"HIP count training: no backward for {type(layer).__name__}")
 
 
 def hip_count_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor,
@@ -425,6 +449,58 @@ def _down_backward(mod: nn.Sequential, sv: dict, dy: Tensor, need_dx: bool) -> O
     return None if dx is None else dx.view(b, h, w, cin)
 
 
+def _addon_suffix_backward(m: nn.Module, feats: Tensor, saved: list, d_logits: Tensor) -> None:
+    """Backward from d logits (before the prototype softmax) through the add-on (1x1 conv when
+    present) and the saved backbone suffix; every parameter with requires_grad gets .grad."""
+    from . import _lib
+    mods = list(m._add_on) if isinstance(m._add_on, nn.Sequential) else [m._add_on]
+    if len(mods) == 2:                           # 1x1 prototype conv before the softmax
+        conv = mods[0]
+        bsz, hh, ww, cf = feats.shape
+        pn = conv.out_channels
+        dl = d_logits.view(-1, pn)
+        if conv.weight.requires_grad:
+            _set_grad(conv.weight, K.wgrad(dl, feats.view(-1, cf)))
+        if conv.bias is not None and conv.bias.requires_grad:
+            _set_grad(conv.bias, K.colsum(dl))
+        dy = K.linear(dl, conv.weight.detach().view(pn, cf).t().contiguous(), None, _lib.EPI_NONE)
+        dy = dy.view(bsz, hh, ww, cf)
+    else:
+        dy = d_logits
+    for i in range(len(saved) - 1, -1, -1):
+        kind, mod, _, sv = saved[i]
+        if kind == "block":
+            dy = _block_backward(mod, sv, dy)
+        else:
+            dy = _down_backward(mod, sv, dy, need_dx=i > 0)
+        saved[i] = None                          # free the activations as we go
+
+
+def _step_train_optimizers(m: nn.Module, optimizer_net, optimizer_classifier, pretrain: bool,
+                           enforce_weight_sparsity: bool) -> None:
+    """optimizer_classifier (not in pretrain; train.py:117-120) and optimizer_net (train.py:122-124)
+    as device AdamW steps, then the sparsity clamps (train.py:131-140)."""
+    cls = m._classification
+    if not pretrain:
+        for g in optimizer_classifier.param_groups:
+            for p in g["params"]:
+                if p.grad is not None:
+                    post = None
+                    if enforce_weight_sparsity:
+                        post = (SPARSITY_DELTA, 0.0) if p is cls.weight else (0.0, 0.0) if p is cls.bias else None
+                    hip_adamw_step(optimizer_classifier, p, p.grad, post)
+    for g in optimizer_net.param_groups:
+        for p in g["params"]:
+            if p.grad is not None:
+                hip_adamw_step(optimizer_net, p, p.grad)
+    if not pretrain and enforce_weight_sparsity:
+        if not cls.weight.requires_grad:
+            K.weight_sparsify_(cls.weight.detach(), SPARSITY_DELTA)
+        if cls.bias is not None and not cls.bias.requires_grad:
+            K.clamp_min_(cls.bias.detach(), 0.0)
+        K.clamp_min_(cls.normalization_multiplier.detach(), 1.0)
+
+
 def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimizer_net, optimizer_classifier,
                    pretrain: bool, epoch: int, nr_epochs: int, enforce_weight_sparsity: bool = True,
                    sd_keep: Optional[Dict[int, Tensor]] = None, generator: Optional[torch.Generator] = None,
@@ -435,7 +511,6 @@ def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimiz
     parameter with requires_grad gets its .grad), then optimizer_classifier (joint only)
     and optimizer_net steps (AdamW on the device) and the sparsity clamps.  Returns the
     loss-kernel stats without synchronising."""
-    from . import _lib
     from .pipnet import add_on_logits_hip
     m = _inner(net)
     j = trainable_suffix_start(m)
@@ -459,46 +534,69 @@ def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimiz
             if cls.bias is not None:
                 _set_grad(cls.bias, db)
         d_logits = K.head_backward(proto, pooled, d_out, cls.weight, w_align, w_tanh)
-        mods = list(m._add_on) if isinstance(m._add_on, nn.Sequential) else [m._add_on]
-        if len(mods) == 2:                           # 1x1 prototype conv before the softmax
-            conv = mods[0]
-            bsz, hh, ww, cf = feats.shape
-            pn = conv.out_channels
-            dl = d_logits.view(-1, pn)
-            if conv.weight.requires_grad:
-                _set_grad(conv.weight, K.wgrad(dl, feats.view(-1, cf)))
-            if conv.bias is not None and conv.bias.requires_grad:
-                _set_grad(conv.bias, K.colsum(dl))
-            dy = K.linear(dl, conv.weight.detach().view(pn, cf).t().contiguous(), None, _lib.EPI_NONE)
-            dy = dy.view(bsz, hh, ww, cf)
-        else:
-            dy = d_logits
-        for i in range(len(saved) - 1, -1, -1):
-            kind, mod, _, sv = saved[i]
-            if kind == "block":
-                dy = _block_backward(mod, sv, dy)
-            else:
-                dy = _down_backward(mod, sv, dy, need_dx=i > 0)
-            saved[i] = None                          # free the activations as we go
+        _addon_suffix_backward(m, feats, saved, d_logits)
         if step_optimizers:
-            if not pretrain:
-                for g in optimizer_classifier.param_groups:
-                    for p in g["params"]:
-                        if p.grad is not None:
-                            post = None
-                            if enforce_weight_sparsity:
-                                post = (SPARSITY_DELTA, 0.0) if p is cls.weight else (0.0, 0.0) if p is cls.bias else None
-                            hip_adamw_step(optimizer_classifier, p, p.grad, post)
-            for g in optimizer_net.param_groups:
-                for p in g["params"]:
-                    if p.grad is not None:
-                        hip_adamw_step(optimizer_net, p, p.grad)
-            if not pretrain and enforce_weight_sparsity:
-                if not cls.weight.requires_grad:
-                    K.weight_sparsify_(cls.weight.detach(), SPARSITY_DELTA)
-                if cls.bias is not None and not cls.bias.requires_grad:
-                    K.clamp_min_(cls.bias.detach(), 0.0)
-                K.clamp_min_(cls.normalization_multiplier.detach(), 1.0)
+            _step_train_optimizers(m, optimizer_net, optimizer_classifier, pretrain, enforce_weight_sparsity)
+    return stats
+
+
+def hip_count_train_supported(net: nn.Module) -> bool:
+    """A ConvNeXt CountPIPNet (fp32, ROCm) whose trainable backbone part is a suffix without
+    the stem, with an intermediate layer that has a HIP backward (the reference's pretrain
+    and "train + freeze params" phases for CountPIPNet, main.py:238-256, 360-390)."""
+    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    m = _inner(net)
+    if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+        return False
+    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, BilinearIntermediate)):
+        return False
+    if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
+        return False
+    return 1 <= trainable_suffix_start(m) < len(m._net.features)
+
+
+def hip_count_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimizer_net, optimizer_classifier,
+                         pretrain: bool, epoch: int, nr_epochs: int, enforce_weight_sparsity: bool = True,
+                         tanh_loss_coeff: float = 1.0, sd_keep: Optional[Dict[int, Tensor]] = None,
+                         generator: Optional[torch.Generator] = None, step_optimizers: bool = True) -> Tensor:
+    """One CountPIPNet pretrain (``pretrain=True``) or joint iteration (train.py:75-140 with
+    is_count_pipnet=True, finetune=False): train-mode forward keeping the backbone suffix's
+    activations (soft Gumbel-softmax / softmax head, spatial sums = raw counts, STE round and
+    clamp, intermediate layer, classifier), the loss kernel (tanh over C * raw counts), then
+    the backward: classifier -> intermediate (parameter and input gradients; ModifiedSTE for
+    a one-hot encoder) -> ClampSTE / STE_Round -> d counts (+ the tanh term) -> d proto
+    (+ the align term) -> soft-max backward scaled by 1/tau -> add-on -> suffix; AdamW steps
+    and the sparsity clamps as ``hip_train_step``.  Returns the loss-kernel stats."""
+    m = _inner(net)
+    j = trainable_suffix_start(m)
+    if not 1 <= j < len(m._net.features):
+        raise NotImplementedError("HIP count training step: needs a trainable backbone suffix without the stem")
+    xs = torch.cat([xs1, xs2])
+    if sd_keep is None:
+        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+    cls = m._classification
+    w_align, w_tanh, w_class = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
+    with torch.no_grad():
+        proto, counts, clamped, saved, inter, out = _count_train_forward(m, xs, sd_keep, j)
+        stats, d_out = K.train_loss(proto, counts, out, ys, cls.normalization_multiplier, enforce_weight_sparsity,
+                                    tanh_loss_coeff, w_align, w_tanh, w_class, "pretrain" if pretrain else "train")
+        d_counts = None
+        if d_out is not None:
+            if cls.weight.requires_grad or (cls.bias is not None and cls.bias.requires_grad):
+                dw, db = K.nonneg_linear_backward(d_out, inter, cls.weight, cls.bias is not None)
+                _set_grad(cls.weight, dw)
+                if cls.bias is not None:
+                    _set_grad(cls.bias, db)
+            d_inter = K.nonneg_linear_dx(d_out, cls.weight.detach())
+            d_clamped = _intermediate_backward(m._intermediate, clamped, saved, d_inter, need_dx=True)
+            if d_clamped is not None:
+                d_counts = K.count_ste_backward(counts, d_clamped, m._max_count, bool(m._use_ste),
+                                                not m._is_clamp_backward_identity or not m._use_ste)
+        d_logits = K.count_head_backward(proto, counts, d_counts, w_align, w_tanh, tanh_loss_coeff, saved["tau"])
+        del proto
+        _addon_suffix_backward(m, saved["feats"], saved["suffix"], d_logits)
+        if step_optimizers:
+            _step_train_optimizers(m, optimizer_net, optimizer_classifier, pretrain, enforce_weight_sparsity)
     return stats
 
 
@@ -568,15 +666,24 @@ def train_pipnet(net, train_loader, optimizer_net, optimizer_classifier, schedul
     run the reference's own loop on these modules (torch autograd path)."""
     if pretrain and finetune:
         raise NotImplementedError("count_pipnet_amd.train_pipnet: pretrain and finetune are exclusive")
-    if is_count_pipnet:
-        if not (finetune and hip_count_finetune_supported(net)):
-            raise NotImplementedError("count_pipnet_amd.train_pipnet: only the CountPIPNet finetune phase has a HIP "
-                                      "step; run the reference train_pipnet with these modules for the others")
+    if is_count_pipnet and finetune:
+        if not hip_count_finetune_supported(net):
+            raise NotImplementedError("count_pipnet_amd.train_pipnet: this CountPIPNet finetune setup has no HIP "
+                                      "step; run the reference train_pipnet with these modules")
         weights = FINETUNE_LOSS_WEIGHTS
 
         def step(a, b, labels):
             return hip_count_finetune_step(net, a, b, labels, optimizer_classifier, enforce_weight_sparsity,
                                            tanh_loss_coeff, generator=generator)
+    elif is_count_pipnet:
+        if not hip_count_train_supported(net):
+            raise NotImplementedError("count_pipnet_amd.train_pipnet: this CountPIPNet training setup (trainable "
+                                      "stem or intermediate without a HIP backward) runs on the torch path")
+        weights = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
+
+        def step(a, b, labels):
+            return hip_count_train_step(net, a, b, labels, optimizer_net, optimizer_classifier, pretrain, epoch,
+                                        nr_epochs, enforce_weight_sparsity, tanh_loss_coeff, generator=generator)
     elif finetune and hip_finetune_supported(net):
         weights = FINETUNE_LOSS_WEIGHTS
 

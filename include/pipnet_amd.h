@@ -374,6 +374,28 @@ int pipnet_head_bwd_f32(const float* proto, const float* pooled, int Bh, int HW,
                         const float* W, int K, float w_align, float w_tanh, float tanh_coeff, int32_t* argmax_ws,
                         float* dpool_ws, float* d_logits, void* stream);
 
+/* ---- CountPIPNet pretrain / joint backward (pipnet/train.py:75-140 with is_count_pipnet;
+ * count_pipnet.py:70-110, count_pipnet_utils.py:41-84, 188-321) ----------------------------
+ * pipnet_count_ste_bwd_f32: d counts_raw from d clamped through STE_Round (identity) and
+ *   ClampSTE(0, max_count) -- gated = 1 ("Gated": pass where the clamp input, rint(counts)
+ *   with use_ste, the raw counts without, lies in [0, max_count]), 0 ("Identity").
+ * pipnet_onehot_ste_bwd_f32: ModifiedSTEFunction.backward over rows = B*P of the encoding
+ *   gradient g [rows][M]; x = the encoder input (clamped counts); strategy 0 = None/'none',
+ *   1 = 'current_grad', 2 = 'max_grad'; flag_ws one int of workspace.  Reproduces the
+ *   reference's effective behaviour (zero-count rows and the non-all-positive rows of a
+ *   'max_grad' batch get 0: its chained mask assignments write temporaries).
+ * pipnet_count_head_bwd_f32: d logits of the count head -- counts = spatial sums of
+ *   proto = softmax((logits + g) * inv_tau) -- for the align (w_align), tanh (w_tanh on
+ *   tanh_coeff * counts) terms plus d_counts_in (NULL or [2Bh][P], the classifier chain);
+ *   proto NHWC [2Bh][HW][P], dcnt_ws float [2Bh*P]. */
+int pipnet_count_ste_bwd_f32(const float* counts, int64_t n, int max_count, int use_ste, int gated,
+                             const float* d_clamped, float* d_counts, void* stream);
+int pipnet_onehot_ste_bwd_f32(const float* x, int64_t rows, int M, const float* g, int strategy, int respect_active,
+                              int* flag_ws, float* dx, void* stream);
+int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, int HW, int P, const float* d_counts_in,
+                              float w_align, float w_tanh, float tanh_coeff, float inv_tau, float* dcnt_ws,
+                              float* d_logits, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,3 +105,44 @@ def finetune_update(pooled: Tensor, out: Tensor, ys1: Tensor, w: Tensor, b: Opti
         res.update(b=torch.clamp(nb, min=0.0) if enforce else nb, b_m=mb, b_v=vb)
     res["mult"] = max(mult, 1.0) if enforce else mult
     return res
+
+
+# ---- CountPIPNet count backward (pretrain / joint phases) ---------------------------------
+def onehot_ste_backward(x, g, strategy=None, respect_active=False):
+    """ModifiedSTEFunction.backward (count_pipnet_utils.py:226-321) restated row by row in
+    numpy: x [B,P] encoder input (clamped counts), g [B,P,M] encoding gradient -> dx [B,P].
+    The reference's effective behaviour: `counts_grad[zero_mask][neg] = ...` (:317-319) and
+    `final_grad_nz[std][dec] = ...` (:279-280) assign into temporaries, so zero-count rows
+    and, in a 'max_grad' batch holding an all-positive row, the other rows get 0."""
+    import numpy as np
+    x = np.asarray(x, dtype=np.float32)
+    g = np.asarray(g, dtype=np.float32).reshape(x.shape + (-1,))
+    m = g.shape[-1]
+    r = np.round(x)                                          # torch.round: half to even
+    nz = ~(r < 0.1)
+    mn, mi, mx = g.min(axis=-1), g.argmin(axis=-1), g.max(axis=-1)   # argmin: first index
+    cur = np.clip(r.astype(np.int64) - 1, 0, m - 1)
+    gcur = np.take_along_axis(g, cur[..., None], axis=-1)[..., 0]
+    allpos = mn > 0
+    dx = np.zeros_like(x)
+    if strategy == "max_grad" and (allpos & nz).any():
+        dx = np.where(allpos, mx, 0.0).astype(np.float32)
+    else:
+        mag = np.abs(mn)
+        if strategy == "current_grad":
+            mag = np.where(allpos, gcur, mag)
+        dx = np.where(mi < cur, mag, np.where(mi > cur, -mag, 0.0)).astype(np.float32)
+    if respect_active:
+        dx = np.where(gcur < 0, 0.0, dx).astype(np.float32)
+    return np.where(nz, dx, 0.0).astype(np.float32)
+
+
+def count_clamp_backward(counts, d_clamped, max_count, use_ste, gated):
+    """d raw counts through STE_Round (identity, count_pipnet_utils.py:52-55) + ClampSTE
+    (:67-84, gate on its input rint(counts)), or torch.clamp on the raw counts without STE
+    (count_pipnet.py:94-96: the train-mode forward does not round)."""
+    import numpy as np
+    c = np.asarray(counts, dtype=np.float32)
+    xin = np.round(c) if use_ste else c
+    keep = (xin >= 0) & (xin <= max_count) if gated else np.ones_like(c, dtype=bool)
+    return np.where(keep, np.asarray(d_clamped, dtype=np.float32), 0.0).astype(np.float32)

@@ -58,6 +58,14 @@ TRAIN_CASES = {
     # noise injected as in gen_golden (synth_exponential, seeds noise_seed + k per forward)
     "train_count_finetune_onehot": ("count_onehot", 3, 3, 306, True, "count_finetune"),
     "train_count_finetune_bilinear": ("count_bilinear_small", 3, 2, 307, True, "count_finetune"),
+    # CountPIPNet pretrain / joint (main.py:238-256, 360-390): the mid-layer suffix + add-on
+    # (+ classifier + intermediate in the joint phase) train; backward through the soft Gumbel
+    # head, STE round / ClampSTE and the intermediate layer (ModifiedSTE for one-hot)
+    "train_count_pretrain_onehot": ("count_onehot", 2, 3, 308, True, "count_pretrain"),
+    "train_count_joint_onehot": ("count_onehot", 3, 3, 309, True, "count_joint"),
+    "train_count_joint_identity": ("c1_count_identity", 2, 3, 310, True, "count_joint"),
+    "train_count_joint_linear_full": ("count_linear_full", 2, 3, 311, True, "count_joint"),
+    "train_count_joint_bilinear": ("count_bilinear_small", 2, 2, 312, True, "count_joint"),
 }
 LR, WD = 0.05, 0.01
 
@@ -88,7 +96,8 @@ def run(name):
     import pipnet.train as ref_train
     from util.args import get_optimizer_nn
     dp = nn.DataParallel(net)
-    count = phase == "count_finetune"
+    count = phase.startswith("count_")
+    base = phase[len("count_"):] if count else phase            # finetune / joint / pretrain
     args = argparse.Namespace(net=case["net"], use_mid_layers=case.get("use_mid_layers", False),
                               num_stages=case.get("num_stages", 2), bias=case["bias"], lr=LR, lr_net=5e-4,
                               lr_block=5e-4, weight_decay=WD, optimizer="Adam", seed=1, train_intermediate=count)
@@ -97,11 +106,11 @@ def run(name):
     for p in net.parameters():                       # main.py:335-339 (finetune)
         p.requires_grad = False
     for p in net._classification.parameters():
-        p.requires_grad = phase != "pretrain"
-    if count and getattr(net, "_intermediate", None) is not None:     # main.py:341-343
+        p.requires_grad = base != "pretrain"
+    if count and getattr(net, "_intermediate", None) is not None:     # main.py:341-343, 251-253, 386-388
         for p in net._intermediate.parameters():
-            p.requires_grad = True
-    if phase not in ("finetune", "count_finetune"):   # main.py:240-249 / 377-385
+            p.requires_grad = base != "pretrain"
+    if base != "finetune":                           # main.py:240-249 / 377-385
         for group in (to_train, to_freeze, list(net._add_on.parameters())):
             for p in group:
                 p.requires_grad = True
@@ -134,10 +143,10 @@ def run(name):
         with injected_bernoulli(seed=5000 + seed) as drawn, G.injected_exponential(seed=7000 + seed) as noise, \
                 contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
             info = ref_train.train_pipnet(dp, batches, opt_net, opt_cls,
-                                          sched_net, None if phase == "pretrain" else sched_cls, criterion,
-                                          1, 2 if phase == "pretrain" else 1, torch.device("cpu"),
-                                          is_count_pipnet=count, pretrain=phase == "pretrain",
-                                          finetune=phase in ("finetune", "count_finetune"),
+                                          sched_net, None if base == "pretrain" else sched_cls, criterion,
+                                          1, 2 if base == "pretrain" else 1, torch.device("cpu"),
+                                          is_count_pipnet=count, pretrain=base == "pretrain",
+                                          finetune=base == "finetune",
                                           enforce_weight_sparsity=True)
     finally:
         h.remove()
@@ -164,7 +173,7 @@ def run(name):
     if count:                    # the trained intermediate tensors, in full (small cases)
         for pname, prm in net._intermediate.named_parameters():
             rec[f"inter/{pname}"] = prm.detach().numpy()
-    if phase not in ("finetune", "count_finetune"):   # every trainable backbone / add-on tensor
+    if base != "finetune":       # every trainable backbone / add-on tensor
         for pname, prm in net.named_parameters():
             if prm.requires_grad and not pname.startswith("_classification"):
                 a = prm.detach().double()

@@ -28,6 +28,7 @@ pytestmark = pytest.mark.gpu
 NAMES = [n for n in train_golden_names() if n.startswith("train_finetune_")]
 SUFFIX = [n for n in train_golden_names() if not n.startswith(("train_finetune_", "train_count_"))]
 COUNT = [n for n in train_golden_names() if n.startswith("train_count_finetune_")]
+COUNT_SUFFIX = [n for n in train_golden_names() if n.startswith(("train_count_joint_", "train_count_pretrain_"))]
 
 
 def _t(a):
@@ -457,4 +458,111 @@ def test_count_train_pipnet_epoch(gpu):
         info = T.train_pipnet(net, batches, opt, opt, None, sched, None, 1, 1, gpu, is_count_pipnet=True,
                               finetune=True)
     assert len(info["lrs_class"]) == len(batches)
+    assert np.isfinite(info["loss"]) and info["loss"] > 0
+
+
+# ---- CountPIPNet pretrain / joint: backbone suffix + add-on (+ classifier + intermediate) ----
+def _count_suffix_setup(name, gpu):
+    meta, rec, fwd_meta = load_train_golden(name)
+    net = build_model(fwd_meta).to(gpu).train()
+    pmeta = dict(meta, phase=meta["phase"][len("count_"):])
+    opt_net, opt_cls, sched_net, sched_cls = _optimizers_like_reference(net, pmeta, fwd_meta)
+    pretrain = pmeta["phase"] == "pretrain"
+    inter = list(net._intermediate.parameters())
+    if inter:                    # train_intermediate=True (util/args.py:318-321); main.py:251-253, 386-388
+        opt_cls.add_param_group({"params": inter, "lr": meta["lr"], "weight_decay": meta["weight_decay"]})
+        for prm in inter:
+            prm.requires_grad = not pretrain
+        sched_cls = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt_cls, T_0=10, eta_min=0.001, T_mult=1)
+    c = fwd_meta["case"]
+    batches = train_loader_batches(c["size"], c["num_classes"], meta["iterations"], meta["batch_per_view"],
+                                   meta["seed"])
+    return meta, rec, fwd_meta, net, opt_net, opt_cls, sched_net, sched_cls, pretrain, batches
+
+
+def _inject_noise(net, meta, rec, i, gpu):
+    from count_pipnet_amd.count_pipnet_utils import GumbelSoftmax
+    from count_pipnet_amd.synthetic import synth_exponential
+    act = list(net._add_on)[-1]
+    if isinstance(act, GumbelSoftmax):
+        act.exp_noise = synth_exponential(tuple(rec[f"s{i}_proto"].shape), meta["noise_seed"] + i).to(gpu)
+
+
+@pytest.mark.parametrize("name", COUNT_SUFFIX)
+def test_count_suffix_training_matches_reference(gpu, name):
+    """The reference's train_pipnet(is_count_pipnet=True) pretrain / joint run replayed on the
+    HIP step (recorded stochastic-depth masks and Gumbel noise): every iteration's loss terms,
+    then every trainable backbone / add-on / intermediate tensor and the classifier."""
+    meta, rec, fwd_meta, net, opt_net, opt_cls, sched_net, sched_cls, pretrain, batches = \
+        _count_suffix_setup(name, gpu)
+    assert T.hip_count_train_supported(net)
+    iters = len(batches)
+    for i, (xs1, xs2, ys) in enumerate(batches):
+        sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
+        _inject_noise(net, meta, rec, i, gpu)
+        opt_net.zero_grad(set_to_none=True)
+        opt_cls.zero_grad(set_to_none=True)
+        stats = T.hip_count_train_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt_net, opt_cls, pretrain, 1,
+                                       2 if pretrain else 1, True, 1.0, sd_keep=sd_keep).cpu()
+        comp = meta["components"][i]
+        assert float(stats[0]) == pytest.approx(comp["align"], rel=2e-3, abs=1e-4)
+        assert float(stats[1]) == pytest.approx(comp["tanh"], rel=2e-3, abs=1e-4)
+        assert float(stats[3]) == pytest.approx(comp["loss"], rel=2e-3, abs=1e-4)
+        if not pretrain:
+            assert float(stats[2]) == pytest.approx(comp["class"], rel=2e-3, abs=1e-4)
+            sched_cls.step(0 + i / iters)
+        sched_net.step()
+    names = [k.split("/")[1] for k in rec if k.startswith("param/") and k.endswith("/sum")]
+    assert names
+    params = dict(net.named_parameters())
+    assert sorted(names) == sorted(n for n, p in params.items() if p.requires_grad
+                                   and not n.startswith("_classification"))
+    lr_max = max(g["lr"] for g in opt_net.param_groups + opt_cls.param_groups)
+    for pname in names:
+        p = params[pname].detach().cpu().double()
+        head = _t(rec[f"param/{pname}/head"]).double()
+        _quorum_close(p.flatten()[:head.numel()], head, 1e-4, 1e-6, frac=0.95,
+                      max_abs=2.5 * meta["iterations"] * lr_max + 1e-6)
+        ref_abs = float(rec[f"param/{pname}/abs"])
+        assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
+    if not pretrain:
+        _quorum_close(net._classification.weight, _t(rec["final_w"]), 1e-4, 1e-5, frac=0.97,
+                      max_abs=4 * meta["lr"] * iters + 1e-6)
+
+
+@pytest.mark.parametrize("name", COUNT_SUFFIX)
+def test_count_suffix_gradients_match_autograd(gpu, name):
+    """HIP gradients of every trainable tensor == torch autograd through the same modules
+    (their torch path in train mode: soft Gumbel-softmax with the same noise, STE_Round,
+    ClampSTE, ModifiedSTEFunction / Bilinear / LinearFull, NonNegLinear)."""
+    meta, rec, fwd_meta, net, opt_net, opt_cls, _, _, pretrain, batches = _count_suffix_setup(name, gpu)
+    xs1, xs2, ys = batches[0]
+    sd_keep = _sd_keep(net, rec["s0_masks"])
+    _inject_noise(net, meta, rec, 0, gpu)
+    T.hip_count_train_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt_net, opt_cls, pretrain, 1,
+                           2 if pretrain else 1, True, 1.0, sd_keep=sd_keep, step_optimizers=False)
+    hip = {n: p.grad.detach().clone() for n, p in net.named_parameters() if p.grad is not None}
+    for p in net.parameters():
+        p.grad = None
+    wa, wt, wc = (0.5, 5.0, 0.0) if pretrain else (5.0, 2.0, 2.0)
+    masks = [_t(m).float().to(gpu) for m in rec["s0_masks"]]
+    ref = _torch_path_grads(net, torch.cat([xs1, xs2]).to(gpu), ys.to(gpu), masks, wa, wt, wc,
+                            float(net._classification.normalization_multiplier[0]))
+    assert set(hip) == set(ref), (sorted(set(hip) ^ set(ref)))
+    for n in sorted(ref):
+        a, b = hip[n].double(), ref[n].double()
+        scale = b.abs().max().item() + 1e-12
+        err = (a - b).abs().max().item() / scale
+        assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"
+
+
+def test_count_train_pipnet_joint_epoch(gpu):
+    """count_pipnet_amd.train_pipnet(is_count_pipnet=True) drives the HIP pretrain / joint steps."""
+    name = [n for n in COUNT_SUFFIX if "joint" in n][0]
+    meta, rec, fwd_meta, net, opt_net, opt_cls, sched_net, sched_cls, pretrain, batches = \
+        _count_suffix_setup(name, gpu)
+    with contextlib.redirect_stdout(io.StringIO()):
+        info = T.train_pipnet(net, batches, opt_net, opt_cls, sched_net, sched_cls, None, 1, 1, gpu,
+                              is_count_pipnet=True)
+    assert len(info["lrs_class"]) == len(batches) and len(info["lrs_net"]) == len(batches)
     assert np.isfinite(info["loss"]) and info["loss"] > 0

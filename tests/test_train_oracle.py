@@ -26,7 +26,8 @@ FINETUNE = [n for n in NAMES if n.startswith("train_finetune_")]
 def _loss_weights(meta):
     """(align, tanh, class) weights of train.py:51-61 for the fixture's phase (epoch 1)."""
     return {"pretrain": (0.5, 5.0, 0.0), "joint": (5.0, 2.0, 2.0), "finetune": (0.0, 0.0, 2.0),
-            "count_finetune": (0.0, 0.0, 2.0)}[meta["phase"]]
+            "count_finetune": (0.0, 0.0, 2.0), "count_pretrain": (0.5, 5.0, 0.0),
+            "count_joint": (5.0, 2.0, 2.0)}[meta["phase"]]
 
 
 def _t(a):
@@ -42,7 +43,7 @@ def test_oracle_loss_terms_match_reference(name):
         proto = _t(rec[f"s{i}_proto"]) if f"s{i}_proto" in rec else torch.zeros(pooled.shape + (1, 1)) + 0.5
         got = train_ref.loss_terms(proto, pooled, out, ys, mult)
         assert float(got["tanh"]) == pytest.approx(comp["tanh"], rel=1e-5, abs=1e-6)
-        if meta["phase"] != "pretrain":
+        if not meta["phase"].endswith("pretrain"):
             assert float(got["cls"]) == pytest.approx(comp["class"], rel=1e-5, abs=1e-6)
             assert float(got["correct"]) / (2 * len(ys)) == comp["acc"]
         wa, wt, wc = _loss_weights(meta)
