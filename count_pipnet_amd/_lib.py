@@ -67,6 +67,7 @@ SIGNATURES = {
     "pipnet_wgrad_workspace_bytes": [I32, I32, I32],
     "pipnet_wgrad_f32": [P, I64, P, I64, I32, I32, I32, P, I64, I32, P, P],
     "pipnet_wgrad_conv2x2_f32": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P, P],
+    "pipnet_wgrad_conv_f32": [P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
     "pipnet_colsum_workspace_bytes": [I32],
     "pipnet_colsum_f32": [P, I64, I32, I32, P, I32, P, P],
     "pipnet_train_partials_floats": [I32],

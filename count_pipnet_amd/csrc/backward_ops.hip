@@ -18,10 +18,11 @@ constexpr int WG_T = 256, WB1 = 128, WB2 = 128, WBK = 32, WPAD = 4;
 constexpr int WLD1 = WB1 + WPAD, WLD2 = WB2 + WPAD;    // padded rows: the two half-waves
                                                          // (k and k+1) hit different banks
 
-// B operand gather of the 2x2 (stride s) downsample conv's weight gradient: row m = output
-// pixel (b, oy, ox), column k = tap * Cin + ci -> input x[b][oy*s + tap/2][ox*s + tap%2][ci].
+// B operand gather of a KHxKW (stride s, no padding) conv's weight gradient -- the 2x2
+// downsample convs and the 4x4/4 stem: row m = output pixel (b, oy, ox), column k =
+// tap * Cin + ci -> input x[b][oy*s + tap/KW][ox*s + tap%KW][ci].
 struct Conv2x2Geom {
-  int H, W, Cin, OH, OW, stride;
+  int H, W, Cin, OH, OW, stride, KW;
 };
 
 template <int BCONV>
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(WG_T, 2) void wgrad_kernel(const float* __restrict_
   int64_t b_tap_off = 0;                              // conv gather: this thread's tap / channel
   if (BCONV) {
     const int k = n2_0 + lc, tap = k / cg.Cin, ci = k - tap * cg.Cin;
-    b_tap_off = ((int64_t)(tap >> 1) * cg.W + (tap & 1)) * cg.Cin + ci;
+    b_tap_off = ((int64_t)(tap / cg.KW) * cg.W + (tap % cg.KW)) * cg.Cin + ci;
   }
   f32x4 ra[4], rb[4];
   auto gload = [&](int m0) {
@@ -179,7 +180,7 @@ int wgrad_launch(const float* A, int64_t lda, const float* B, int64_t ldb, int M
   if (!direct && !workspace) return PIPNET_ERR_ARG;
   float* out = direct ? C : workspace;
   const int64_t ldo = direct ? ldc : N2;
-  const Conv2x2Geom g = cg ? *cg : Conv2x2Geom{0, 0, 1, 0, 0, 1};
+  const Conv2x2Geom g = cg ? *cg : Conv2x2Geom{0, 0, 1, 0, 0, 1, 1};
   if (cg)
     hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)tiles, (unsigned)splits), dim3(WG_T), 0, s, A, lda, B, ldb, M,
                        N1, N2, mchunk, t2n, out, ldo, (int64_t)N1 * N2, g);
@@ -213,9 +214,23 @@ extern "C" int pipnet_wgrad_conv2x2_f32(const float* dY, const float* x, int B, 
   if (!dY || !x || !dW) return PIPNET_ERR_ARG;
   if (!aligned16(dY) || !aligned16(x)) return PIPNET_ERR_ALIGN;
   const int OH = (H - 2) / stride + 1, OW = (W - 2) / stride + 1;
-  const Conv2x2Geom g{H, W, Cin, OH, OW, stride};
+  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, 2};
   return wgrad_launch(dY, Cout, x, 4 * Cin, B * OH * OW, Cout, 4 * Cin, dW, 4 * Cin, accumulate, workspace,
                       (hipStream_t)stream, &g);
+}
+
+extern "C" int pipnet_wgrad_conv_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int KH, int KW,
+                                     int stride, int Cout, float* dW, int accumulate, float* workspace,
+                                     void* stream) {
+  if (B <= 0 || KH <= 0 || KW <= 0 || H < KH || W < KW || Cin <= 0 || Cout <= 0 || (Cin & 3) || (Cout & 3) ||
+      stride <= 0)
+    return PIPNET_ERR_ARG;
+  if (!dY || !x || !dW) return PIPNET_ERR_ARG;
+  if (!aligned16(dY) || !aligned16(x)) return PIPNET_ERR_ALIGN;
+  const int OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1;
+  const int K = KH * KW * Cin;
+  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, KW};
+  return wgrad_launch(dY, Cout, x, K, B * OH * OW, Cout, K, dW, K, accumulate, workspace, (hipStream_t)stream, &g);
 }
 
 extern "C" int pipnet_colsum_workspace_bytes(int N) { return N > 0 ? CS_SPLITS * N * (int)sizeof(float) : 0; }

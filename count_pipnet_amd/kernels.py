@@ -855,6 +855,23 @@ def dwconv7_wgrad(dz_nhwc: Tensor, x_nhwc: Tensor, dw_packed: Tensor, db: Tensor
               db.data_ptr(), int(accumulate), _partials(c, x_nhwc.device).data_ptr(), _stream(x_nhwc))
 
 
+def wgrad_conv(dy_nhwc: Tensor, x_nhwc: Tensor, kh: int, kw: int, stride: int, out: Tensor,
+               accumulate: bool = False) -> Tensor:
+    """Packed [Cout, KH*KW*Cin] weight gradient of a KHxKW conv (stride, no padding)."""
+    _chk(dy_nhwc, "d conv output")
+    _chk(x_nhwc, "conv input")
+    b, h, w, cin = x_nhwc.shape
+    cout = dy_nhwc.shape[-1]
+    oh, ow = (h - kh) // stride + 1, (w - kw) // stride + 1
+    if tuple(dy_nhwc.shape) != (b, oh, ow, cout) or out.numel() != cout * kh * kw * cin:
+        raise RuntimeError(f"wgrad_conv: dY {tuple(dy_nhwc.shape)}, x {tuple(x_nhwc.shape)}, k{kh}x{kw}/{stride}")
+    nbytes = _lib.load().pipnet_wgrad_workspace_bytes(b * oh * ow, cout, kh * kw * cin)
+    ws = torch.empty(max(nbytes // 4, 1), device=x_nhwc.device, dtype=torch.float32)
+    _lib.call("pipnet_wgrad_conv_f32", dy_nhwc.data_ptr(), x_nhwc.data_ptr(), b, h, w, cin, kh, kw, stride, cout,
+              out.data_ptr(), int(accumulate), ws.data_ptr(), _stream(x_nhwc))
+    return out
+
+
 def wgrad_conv2x2(dy_nhwc: Tensor, x_nhwc: Tensor, stride: int, out: Tensor, accumulate: bool = False) -> Tensor:
     """Packed [Cout, 4*Cin] weight gradient of the 2x2 downsample conv."""
     b, h, w, cin = x_nhwc.shape

@@ -326,14 +326,15 @@ def trainable_suffix_start(net: nn.Module) -> int:
 
 
 def hip_train_supported(net: nn.Module) -> bool:
-    """A ConvNeXt PIP-Net (fp32, ROCm) whose trainable backbone part is a suffix that does
-    not include the stem (the reference's pretrain / frozen phases)."""
+    """A ConvNeXt PIP-Net (fp32, ROCm) whose trainable backbone part is a suffix features[j:]
+    (the reference's pretrain / "train + freeze params" phases; j = 0, the stem included: the
+    "train everything" epochs after freeze_epochs, main.py:362-373)."""
     m = _inner(net)
     if hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
-    return trainable_suffix_start(m) >= 1
+    return trainable_suffix_start(m) < len(m._net.features)
 
 
 def _forward_saving(m: nn.Module, xs: Tensor, j: int, sd_keep: Dict[int, Tensor]):
@@ -344,11 +345,24 @@ def _forward_saving(m: nn.Module, xs: Tensor, j: int, sd_keep: Dict[int, Tensor]
     from . import _lib
     from .convnext_features import LayerNorm2d, packed, stochastic_depth_row_scales
     feats, cache = m._net.features, m._net._hip_pack
-    h = convnext_features_hip(feats[:j], xs, cache, sd_keep)
-    scales = stochastic_depth_row_scales(feats, sd_keep, xs.shape[0], xs.device)
     saved = []
-    bid = len(_cnblocks(feats[:j]))
-    for idx in range(j, len(feats)):
+    if j == 0:       # trainable stem (the "train everything" epochs): conv k4 s4 and LN unfused
+        conv, ln = feats[0][0], feats[0][1]
+        if conv.kernel_size != (4, 4) or conv.stride != (4, 4) or conv.in_channels != 3 or conv.padding != (0, 0):
+            raise RuntimeError(f"HIP training step: unsupported ConvNeXt stem {conv}")
+        xp = K.nchw_to_nhwc(xs.contiguous(), 4)                     # channels zero-padded 3 -> 4
+        wp = packed(cache, "0.conv.train", conv.weight,
+                    lambda w: torch.nn.functional.pad(w.permute(0, 2, 3, 1), (0, 1)))
+        z = K.conv2d_nhwc(xp, wp, conv.bias, 4, 0, _lib.EPI_BIAS)
+        h = K.layernorm(z, ln.weight, ln.bias)
+        saved.append(("stem", feats[0], "0", dict(x=xp, z=z)))
+        start = 1
+    else:
+        h = convnext_features_hip(feats[:j], xs, cache, sd_keep)
+        start = j
+    scales = stochastic_depth_row_scales(feats, sd_keep, xs.shape[0], xs.device)
+    bid = len(_cnblocks(feats[:start]))
+    for idx in range(start, len(feats)):
         mod = feats[idx]
         if len(mod) > 0 and isinstance(mod[0], CNBlock):
             for jb, blk in enumerate(mod):
@@ -417,6 +431,28 @@ def _block_backward(blk: CNBlock, sv: dict, dy: Tensor) -> Tensor:
     return dx
 
 
+def _stem_backward(mod: nn.Sequential, sv: dict, dy: Tensor) -> None:
+    """Stem backward (Conv2d(3, 96, 4, 4) + LayerNorm2d): LN gradients, then the conv's
+    weight (stride-4 patch gather, MFMA) and bias gradients; the input images need none."""
+    conv, ln = mod[0], mod[1]
+    z = sv["z"]
+    b, h, w, c = z.shape
+    dev = z.device
+    d_lnw, d_lnb = torch.empty(c, device=dev), torch.empty(c, device=dev)
+    need_dz = conv.weight.requires_grad or (conv.bias is not None and conv.bias.requires_grad)
+    dz = K.ln_backward(z.view(-1, c), dy.reshape(-1, c), ln.weight, d_lnw, d_lnb, want_dz=need_dz)
+    _set_grad(ln.weight, d_lnw)
+    _set_grad(ln.bias, d_lnb)
+    if not need_dz:
+        return
+    if conv.weight.requires_grad:
+        gp = torch.empty(c, 4 * 4 * 4, device=dev)
+        K.wgrad_conv(dz.view(b, h, w, c), sv["x"], 4, 4, 4, gp)
+        _set_grad(conv.weight, gp.view(c, 4, 4, 4)[..., :3].permute(0, 3, 1, 2))
+    if conv.bias is not None and conv.bias.requires_grad:
+        _set_grad(conv.bias, K.colsum(dz))
+
+
 def _down_backward(mod: nn.Sequential, sv: dict, dy: Tensor, need_dx: bool) -> Optional[Tensor]:
     """LayerNorm2d + Conv2d(k2, stride 1|2) backward; returns d input when ``need_dx``."""
     from . import _lib
@@ -471,6 +507,8 @@ def _addon_suffix_backward(m: nn.Module, feats: Tensor, saved: list, d_logits: T
         kind, mod, _, sv = saved[i]
         if kind == "block":
             dy = _block_backward(mod, sv, dy)
+        elif kind == "stem":
+            _stem_backward(mod, sv, dy)
         else:
             dy = _down_backward(mod, sv, dy, need_dx=i > 0)
         saved[i] = None                          # free the activations as we go
@@ -514,8 +552,8 @@ def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimiz
     from .pipnet import add_on_logits_hip
     m = _inner(net)
     j = trainable_suffix_start(m)
-    if j < 1:
-        raise NotImplementedError("HIP training step: the ConvNeXt stem is trainable (not supported)")
+    if j >= len(m._net.features):
+        raise NotImplementedError("HIP training step: no trainable backbone parameter (use the finetune step)")
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
         sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
@@ -541,9 +579,10 @@ def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimiz
 
 
 def hip_count_train_supported(net: nn.Module) -> bool:
-    """A ConvNeXt CountPIPNet (fp32, ROCm) whose trainable backbone part is a suffix without
-    the stem, with an intermediate layer that has a HIP backward (the reference's pretrain
-    and "train + freeze params" phases for CountPIPNet, main.py:238-256, 360-390)."""
+    """A ConvNeXt CountPIPNet (fp32, ROCm) whose trainable backbone part is a suffix
+    features[j:] (j = 0: the stem too), with an intermediate layer that has a HIP backward
+    (the reference's pretrain, "train + freeze params" and "train everything" phases for
+    CountPIPNet, main.py:238-256, 360-390)."""
     from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
     m = _inner(net)
     if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
@@ -552,7 +591,7 @@ def hip_count_train_supported(net: nn.Module) -> bool:
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
-    return 1 <= trainable_suffix_start(m) < len(m._net.features)
+    return trainable_suffix_start(m) < len(m._net.features)
 
 
 def hip_count_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimizer_net, optimizer_classifier,
@@ -569,8 +608,8 @@ def hip_count_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, o
     and the sparsity clamps as ``hip_train_step``.  Returns the loss-kernel stats."""
     m = _inner(net)
     j = trainable_suffix_start(m)
-    if not 1 <= j < len(m._net.features):
-        raise NotImplementedError("HIP count training step: needs a trainable backbone suffix without the stem")
+    if j >= len(m._net.features):
+        raise NotImplementedError("HIP count training step: no trainable backbone parameter (use the finetune step)")
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
         sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)

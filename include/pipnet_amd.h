@@ -336,6 +336,12 @@ int pipnet_wgrad_f32(const float* A, int64_t lda, const float* B, int64_t ldb, i
  *   [B,H,W,Cin]; workspace: pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, 4*Cin) bytes. */
 int pipnet_wgrad_conv2x2_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int stride, int Cout,
                              float* dW, int accumulate, float* workspace, void* stream);
+/* pipnet_wgrad_conv_f32: weight gradient of a KHxKW conv, stride s, no padding (the ConvNeXt
+ * stem, torchvision Conv2dNormActivation(3, 96, 4, 4) with Cin zero-padded to 4): dY NHWC
+ * [B][OH][OW][Cout], x NHWC [B][H][W][Cin] -> dW [Cout][KH][KW][Cin] (accumulate adds);
+ * workspace: pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, KH*KW*Cin). */
+int pipnet_wgrad_conv_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int KH, int KW, int stride,
+                          int Cout, float* dW, int accumulate, float* workspace, void* stream);
 int pipnet_colsum_workspace_bytes(int N);
 int pipnet_colsum_f32(const float* A, int64_t lda, int M, int N, float* out, int accumulate, float* workspace,
                       void* stream);

@@ -66,6 +66,11 @@ TRAIN_CASES = {
     "train_count_joint_identity": ("c1_count_identity", 2, 3, 310, True, "count_joint"),
     "train_count_joint_linear_full": ("count_linear_full", 2, 3, 311, True, "count_joint"),
     "train_count_joint_bilinear": ("count_bilinear_small", 2, 2, 312, True, "count_joint"),
+    # "train everything" epochs (main.py:362-373, epoch > freeze_epochs): the whole backbone,
+    # stem included, + add-on + classifier (+ intermediate) train
+    "train_full_mid_addon": ("pipnet_mid_addon", 2, 3, 313, True, "full"),
+    "train_full_c2": ("c2_pipnet_convnext26", 2, 2, 314, False, "full"),
+    "train_count_full_onehot": ("count_onehot", 2, 3, 315, True, "count_full"),
 }
 LR, WD = 0.05, 0.01
 
@@ -114,6 +119,9 @@ def run(name):
         for group in (to_train, to_freeze, list(net._add_on.parameters())):
             for p in group:
                 p.requires_grad = True
+    if base == "full":                               # main.py:362-373
+        for p in backbone:
+            p.requires_grad = True
     net._classification.normalization_multiplier.requires_grad = False
     sched_net = torch.optim.lr_scheduler.CosineAnnealingLR(opt_net, T_max=10, eta_min=5e-6)
     sched_cls = torch.optim.lr_scheduler.CosineAnnealingWarmRestarts(opt_cls, T_0=10, eta_min=0.001, T_mult=1)

@@ -28,7 +28,8 @@ pytestmark = pytest.mark.gpu
 NAMES = [n for n in train_golden_names() if n.startswith("train_finetune_")]
 SUFFIX = [n for n in train_golden_names() if not n.startswith(("train_finetune_", "train_count_"))]
 COUNT = [n for n in train_golden_names() if n.startswith("train_count_finetune_")]
-COUNT_SUFFIX = [n for n in train_golden_names() if n.startswith(("train_count_joint_", "train_count_pretrain_"))]
+COUNT_SUFFIX = [n for n in train_golden_names()
+                if n.startswith(("train_count_joint_", "train_count_pretrain_", "train_count_full_"))]
 
 
 def _t(a):
@@ -270,7 +271,7 @@ def _optimizers_like_reference(net, meta, fwd_meta):
     opt_cls = torch.optim.AdamW(groups, lr=meta["lr"], weight_decay=0.0)
     for prm in net.parameters():
         prm.requires_grad = False
-    for prm in train + freeze + list(net._add_on.parameters()):
+    for prm in train + freeze + list(net._add_on.parameters()) + (backbone if meta["phase"] == "full" else []):
         prm.requires_grad = True
     for prm in cls.parameters():
         prm.requires_grad = meta["phase"] != "pretrain"

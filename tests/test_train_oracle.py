@@ -27,7 +27,7 @@ def _loss_weights(meta):
     """(align, tanh, class) weights of train.py:51-61 for the fixture's phase (epoch 1)."""
     return {"pretrain": (0.5, 5.0, 0.0), "joint": (5.0, 2.0, 2.0), "finetune": (0.0, 0.0, 2.0),
             "count_finetune": (0.0, 0.0, 2.0), "count_pretrain": (0.5, 5.0, 0.0),
-            "count_joint": (5.0, 2.0, 2.0)}[meta["phase"]]
+            "count_joint": (5.0, 2.0, 2.0), "full": (5.0, 2.0, 2.0), "count_full": (5.0, 2.0, 2.0)}[meta["phase"]]
 
 
 def _t(a):
