@@ -15,10 +15,10 @@ GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 def golden_names():
     """Forward golden cases (eval_* fixtures belong to the eval_pipnet metric loop, input_*
-    to the input transform, tests/test_input_oracle.py, train_* to the finetune iteration,
-    tests/test_train_oracle.py)."""
+    to the input transform, tests/test_input_oracle.py, train_* to the training iterations,
+    tests/test_train_oracle.py, count_ste_bwd to the STE backward, tests/test_count_ste.py)."""
     return sorted(f[:-4] for f in os.listdir(GOLDEN_DIR)
-                  if f.endswith(".npz") and not f.startswith(("eval_", "input_", "train_")))
+                  if f.endswith(".npz") and not f.startswith(("eval_", "input_", "train_", "count_ste_")))
 
 
 def eval_golden_names():
