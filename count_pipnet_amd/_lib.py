@@ -37,6 +37,8 @@ SIGNATURES = {
     "pipnet_count_gumbel_soft_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_nonneg_linear_dx_f32": [P, P, I32, I32, I32, P, P],
     "pipnet_bilinear_bwd_prep_f32": [P, P, P, I64, P, P, P],
+    "pipnet_linear_inter_partials_floats": [I32],
+    "pipnet_linear_inter_bwd_f32": [P, I64, I32, P, P, P, P, I32, P, P],
     "pipnet_count_ste_bwd_f32": [P, I64, I32, I32, I32, P, P, P],
     "pipnet_onehot_ste_bwd_f32": [P, I64, I32, P, I32, I32, P, P, P],
     "pipnet_count_head_bwd_f32": [P, P, I32, I32, I32, P, F32, F32, F32, F32, P, P, P],

@@ -220,6 +220,58 @@ __global__ __launch_bounds__(256) void bilinear_bwd_prep_kernel(const float* __r
   }
 }
 
+// LinearIntermediate backward (count_pipnet_utils.py:471-519: out[n][e] = w[e] * x[n] for the
+// rows n = (b, p), e < E, Linear(1, E, bias=False)): dx[n] = sum_e g[n][e] w[e] and per-
+// workgroup partial sums of dw[e] = sum_n g[n][e] x[n] (fixed grid LI_BLOCKS, fixed lane /
+// wave order), reduced in order by linear_inter_dw_kernel -> deterministic.
+constexpr int LI_T = 256, LI_BLOCKS = 512, LI_EMAX = 16;
+
+template <int E>
+__global__ __launch_bounds__(LI_T) void linear_inter_bwd_kernel(const float* __restrict__ x,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ w, int64_t n,
+                                                                float* __restrict__ dx,
+                                                                float* __restrict__ partial) {
+  float wr[E], acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) { wr[e] = w[e]; acc[e] = 0.f; }
+  for (int64_t i = (int64_t)blockIdx.x * LI_T + threadIdx.x; i < n; i += (int64_t)LI_BLOCKS * LI_T) {
+    const float xi = x[i];
+    const float* gi = g + i * E;
+    float d = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float ge = gi[e];
+      d = fmaf(ge, wr[e], d);
+      acc[e] = fmaf(ge, xi, acc[e]);
+    }
+    if (dx) dx[i] = d;
+  }
+  __shared__ float red[LI_T / 64][E];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float v = acc[e];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[wv][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < E) {
+    float v = 0.f;
+    for (int k = 0; k < LI_T / 64; ++k) v += red[k][threadIdx.x];
+    partial[(int64_t)blockIdx.x * E + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(64) void linear_inter_dw_kernel(const float* __restrict__ partial, int E,
+                                                             float* __restrict__ dw, int accumulate) {
+  const int e = threadIdx.x;
+  if (e >= E) return;
+  float v = 0.f;
+  for (int b = 0; b < LI_BLOCKS; ++b) v += partial[(int64_t)b * E + e];
+  dw[e] = accumulate ? dw[e] + v : v;
+}
+
 // torch.optim.AdamW (decoupled weight decay, amsgrad off), one parameter tensor, in torch's
 // float arithmetic (the host turns the double hyper-parameters into the same float
 // constants torch's foreach kernels receive: 1 - lr*wd, 1 - beta1, beta2, 1 - beta2, ...):
@@ -332,6 +384,28 @@ extern "C" int pipnet_bilinear_bwd_prep_f32(const float* g, const float* u, cons
   if (n == 0) return PIPNET_OK;
   hipLaunchKernelGGL(bilinear_bwd_prep_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, g, u, v, n, du,
                      dv);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_linear_inter_partials_floats(int E) { return E > 0 ? LI_BLOCKS * E : 0; }
+
+extern "C" int pipnet_linear_inter_bwd_f32(const float* x, int64_t n, int E, const float* g, const float* w,
+                                           float* dx, float* dw, int accumulate, float* partial, void* stream) {
+  if (n < 0 || E <= 0 || E > LI_EMAX || !x || !g || !w || !dw || !partial) return PIPNET_ERR_ARG;
+  const hipStream_t s = (hipStream_t)stream;
+  switch (E) {
+#define LI_CASE(EE)                                                                                             \
+  case EE:                                                                                                      \
+    hipLaunchKernelGGL(linear_inter_bwd_kernel<EE>, dim3(LI_BLOCKS), dim3(LI_T), 0, s, x, g, w, n, dx, partial); \
+    break;
+    LI_CASE(1) LI_CASE(2) LI_CASE(3) LI_CASE(4) LI_CASE(5) LI_CASE(6) LI_CASE(7) LI_CASE(8)
+    LI_CASE(9) LI_CASE(10) LI_CASE(11) LI_CASE(12) LI_CASE(13) LI_CASE(14) LI_CASE(15) LI_CASE(16)
+#undef LI_CASE
+    default: return PIPNET_ERR_ARG;
+  }
+  PIPNET_CHECK_LAUNCH();
+  hipLaunchKernelGGL(linear_inter_dw_kernel, dim3(1), dim3(64), 0, s, partial, E, dw, accumulate);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

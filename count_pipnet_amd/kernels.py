@@ -545,6 +545,25 @@ def onehot_ste_backward(x: Tensor, g: Tensor, strategy: Optional[str] = None, re
     return dx
 
 
+def linear_intermediate_backward(x: Tensor, g: Tensor, w: Tensor, want_dx: bool = True,
+                                 dw_out: Optional[Tensor] = None) -> Tuple[Optional[Tensor], Tensor]:
+    """LinearIntermediate backward (count_pipnet_utils.py:471-519): x [B,P] counts, g [B,P*E]
+    output gradient, w [E,1] -> (d x [B,P] or None, d w [E,1])."""
+    _chk(x, "intermediate input")
+    _chk(g, "intermediate output gradient")
+    e = w.numel()
+    if g.numel() != x.numel() * e or g.shape[0] != x.shape[0]:
+        raise RuntimeError(f"linear_intermediate_backward: x {tuple(x.shape)}, grad {tuple(g.shape)}, E={e}")
+    wv = w.detach().reshape(-1).contiguous()
+    dx = torch.empty_like(x) if want_dx else None
+    dw = torch.empty(e, 1, device=x.device, dtype=torch.float32) if dw_out is None else dw_out
+    part = torch.empty(int(_lib.load().pipnet_linear_inter_partials_floats(e)), device=x.device,
+                       dtype=torch.float32)
+    _lib.call("pipnet_linear_inter_bwd_f32", x.data_ptr(), x.numel(), e, g.data_ptr(), wv.data_ptr(),
+              dx.data_ptr() if dx is not None else None, dw.data_ptr(), 0, part.data_ptr(), _stream(x))
+    return dx, dw
+
+
 def count_head_backward(proto_nhwc: Tensor, counts: Tensor, d_counts: Optional[Tensor], w_align: float,
                         w_tanh: float, tanh_coeff: float, tau: float) -> Tensor:
     """d loss / d logits of the CountPIPNet head (soft Gumbel-softmax / softmax, spatial sum)

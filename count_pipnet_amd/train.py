@@ -162,11 +162,13 @@ def hip_count_finetune_supported(net: nn.Module) -> bool:
     """A ConvNeXt CountPIPNet (fp32, ROCm) whose trainable parameters are within the
     classifier and an intermediate layer with a HIP backward (identity, one-hot, linear_full,
     bilinear)."""
-    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    from .count_pipnet_utils import (BilinearIntermediate, IdentityIntermediate, LinearFull, LinearIntermediate,
+                                     OneHotEncoder)
     m = _inner(net)
     if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
         return False
-    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, BilinearIntermediate)):
+    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, LinearIntermediate,
+                                       BilinearIntermediate)):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
@@ -228,7 +230,8 @@ def _intermediate_backward(layer: nn.Module, x: Tensor, saved: dict, d_inter: Te
     ``need_dx``, the gradient w.r.t. its input x (the clamped counts) -- None where no gradient
     flows (a OneHotEncoder without STE: create_modified_encoding is not differentiable)."""
     from . import _lib
-    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    from .count_pipnet_utils import (BilinearIntermediate, IdentityIntermediate, LinearFull, LinearIntermediate,
+                                     OneHotEncoder)
     if isinstance(layer, IdentityIntermediate):
         return d_inter if need_dx else None
     if isinstance(layer, OneHotEncoder):
@@ -242,6 +245,14 @@ def _intermediate_backward(layer: nn.Module, x: Tensor, saved: dict, d_inter: Te
         if layer.linear.bias is not None and layer.linear.bias.requires_grad:
             _set_grad(layer.linear.bias, K.colsum(d_inter))
         return K.linear(d_inter, w.detach().t().contiguous(), None, _lib.EPI_NONE) if need_dx else None
+    if isinstance(layer, LinearIntermediate):
+        w = layer.linear.weight
+        if not (w.requires_grad or need_dx):
+            return None
+        dx, dw = K.linear_intermediate_backward(x, d_inter, w, want_dx=need_dx)
+        if w.requires_grad:
+            _set_grad(w, dw.view_as(w))
+        return dx
     if isinstance(layer, BilinearIntermediate):
         e, u, v = saved["e"], saved["u"], saved["v"]
         du, dv = K.bilinear_bwd_prep(d_inter, u, v)
@@ -583,11 +594,13 @@ def hip_count_train_supported(net: nn.Module) -> bool:
     features[j:] (j = 0: the stem too), with an intermediate layer that has a HIP backward
     (the reference's pretrain, "train + freeze params" and "train everything" phases for
     CountPIPNet, main.py:238-256, 360-390)."""
-    from .count_pipnet_utils import BilinearIntermediate, IdentityIntermediate, LinearFull, OneHotEncoder
+    from .count_pipnet_utils import (BilinearIntermediate, IdentityIntermediate, LinearFull, LinearIntermediate,
+                                     OneHotEncoder)
     m = _inner(net)
     if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
         return False
-    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, BilinearIntermediate)):
+    if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, LinearIntermediate,
+                                       BilinearIntermediate)):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
@@ -716,8 +729,8 @@ def train_pipnet(net, train_loader, optimizer_net, optimizer_classifier, schedul
                                            tanh_loss_coeff, generator=generator)
     elif is_count_pipnet:
         if not hip_count_train_supported(net):
-            raise NotImplementedError("count_pipnet_amd.train_pipnet: this CountPIPNet training setup (trainable "
-                                      "stem or intermediate without a HIP backward) runs on the torch path")
+            raise NotImplementedError("count_pipnet_amd.train_pipnet: this CountPIPNet training setup (ResNet "
+                                      "backbone or non-fp32 parameters) runs on the torch path")
         weights = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
 
         def step(a, b, labels):

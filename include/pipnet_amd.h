@@ -140,6 +140,13 @@ int pipnet_nonneg_linear_dx_f32(const float* d_out, const float* W, int N, int D
 int pipnet_bilinear_bwd_prep_f32(const float* g, const float* u, const float* v, int64_t n, float* du, float* dv,
                                  void* stream);
 
+/* LinearIntermediate backward (count_pipnet_utils.py:471-519, Linear(1, E, bias=False) over
+ * the counts x [n = B*P]): g [n][E] -> dx [n] = g w (dx may be NULL) and dw [E] = g^T x
+ * (accumulate adds); partial: pipnet_linear_inter_partials_floats(E) floats; E <= 16. */
+int pipnet_linear_inter_partials_floats(int E);
+int pipnet_linear_inter_bwd_f32(const float* x, int64_t n, int E, const float* g, const float* w, float* dx,
+                                float* dw, int accumulate, float* partial, void* stream);
+
 /* ---- split-bf16 ("bf16x3") fp32 path of the ConvNeXt backbone -------------------------
  * An fp32 operand x is carried as two bf16 values, hi = RNE(x) and lo = RNE(x - hi)
  * (x = hi + lo to ~2^-17 relative).  A product x.w is then hi.hi + lo.hi + hi.lo (the

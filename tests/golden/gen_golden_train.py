@@ -66,6 +66,9 @@ TRAIN_CASES = {
     "train_count_joint_identity": ("c1_count_identity", 2, 3, 310, True, "count_joint"),
     "train_count_joint_linear_full": ("count_linear_full", 2, 3, 311, True, "count_joint"),
     "train_count_joint_bilinear": ("count_bilinear_small", 2, 2, 312, True, "count_joint"),
+    # LinearIntermediate (Linear(1, max_count) per count): finetune and joint phases
+    "train_count_finetune_linear": ("count_linear", 3, 3, 316, True, "count_finetune"),
+    "train_count_joint_linear": ("count_linear", 2, 3, 317, True, "count_joint"),
     # "train everything" epochs (main.py:362-373, epoch > freeze_epochs): the whole backbone,
     # stem included, + add-on + classifier (+ intermediate) train
     "train_full_mid_addon": ("pipnet_mid_addon", 2, 3, 313, True, "full"),

@@ -567,3 +567,31 @@ def test_count_train_pipnet_joint_epoch(gpu):
                               is_count_pipnet=True)
     assert len(info["lrs_class"]) == len(batches) and len(info["lrs_net"]) == len(batches)
     assert np.isfinite(info["loss"]) and info["loss"] > 0
+
+
+@pytest.mark.parametrize("b,p,e,want_dx", [(1, 1, 1, True), (4, 16, 3, True), (7, 2048, 3, False),
+                                           (256, 2048, 3, True), (3, 33, 16, True)])
+def test_linear_intermediate_backward_matches_autograd(gpu, b, p, e, want_dx):
+    """pipnet_linear_inter_bwd_f32 == torch autograd of the reference's LinearIntermediate
+    (count_pipnet_utils.py:471-519): d counts and d weight, ragged row counts, E = 1..16."""
+    from count_pipnet_amd.count_pipnet_utils import LinearIntermediate
+    g0 = torch.Generator().manual_seed(b * 1000 + p + e)
+    layer = LinearIntermediate(p, e).to(gpu)
+    with torch.no_grad():
+        layer.linear.weight.copy_(torch.randn(e, 1, generator=g0))
+    x = torch.randint(0, e + 1, (b, p), generator=g0).float().to(gpu)
+    g = torch.randn(b, p * e, generator=g0).to(gpu)
+    xr = x.clone().requires_grad_(True)
+    layer(xr).backward(g)
+    dx, dw = K.linear_intermediate_backward(x, g, layer.linear.weight, want_dx=want_dx)
+    torch.cuda.synchronize()
+    ref_dw = layer.linear.weight.grad
+    assert dw.shape == ref_dw.shape
+    tol = 1e-5 * (b * p) ** 0.5 * float(g.abs().max() * x.abs().max()) + 1e-6
+    assert (dw - ref_dw).abs().max().item() <= tol
+    if want_dx:
+        assert torch.allclose(dx, xr.grad, rtol=1e-6, atol=1e-6)
+    else:
+        assert dx is None
+    dw2 = K.linear_intermediate_backward(x, g, layer.linear.weight, want_dx=False)[1]
+    assert torch.equal(dw, dw2)                     # deterministic reduction
