@@ -62,6 +62,8 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
     if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
+    else if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2, 0, true>), grid, \
+                                                   block, 0, s, p);                                         \
     else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2>), grid, block, 0, s, p); \
     else if (v == 3) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 2, E, ALOAD, 2, 2>), grid, block, 0, s, p); \
     else hipLaunchKernelGGL((gemm_f32_tn_ktail_kernel<E, ALOAD>), grid, block, 0, s, p);                   \

@@ -358,15 +358,18 @@ PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int
   }
 }
 
-template <int TM>
-PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
+// NPAD: jl (wave-uniform, in an SGPR) = how many of the wave's two 32-column blocks hold
+// columns < N; the MFMAs of a block entirely past N are skipped (N % 128 != 0 grids).
+template <int TM, bool NPAD = false>
+PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f, int jl = 2) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
+        if (!NPAD || j < jl)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
 }
 
 PIPNET_DEV void dma16(const float* src, float* lds_base) {
@@ -385,7 +388,10 @@ PIPNET_DEV void wait_dma_barrier() {
 // ABL (tuning-lab ablations only, 0 in the product): 1 = no DMA (stale LDS), 2 = no
 // epilogue (one store per lane keeps the accumulators live), 4 = no barrier, 8 = stamps.
 // NS = LDS stages: tile k+NS-1 is in flight while tile k is multiplied.
-template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0>
+// NPAD (grids whose N % 128 != 0): MFMA blocks of columns >= N are skipped, and the wave ->
+// column-half map flips with the workgroup parity, so the lighter waves of co-resident
+// workgroups land on different SIMDs (a relabelling: every output is computed identically).
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false>
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
   using G = Geo<BK, TM>;
   // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
@@ -400,10 +406,11 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid >> 1, wn = NPAD ? ((wid & 1) ^ (int)(blockIdx.x & 1)) : (wid & 1);
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
   tile_coords(p, G::BMT, m0, n0);
+  const int jl = NPAD ? __builtin_amdgcn_readfirstlane(min(2, max(0, (p.N - n0 - wn * 64 + 31) >> 5))) : 2;
   if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
 
@@ -470,19 +477,19 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     }
     if constexpr (G::NGROUPS == 4) {
       read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<TM>(acc, fa);
+      mfma_frag<TM, NPAD>(acc, fa, jl);
       read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
-      mfma_frag<TM>(acc, fb);
+      mfma_frag<TM, NPAD>(acc, fb, jl);
       read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
-      mfma_frag<TM>(acc, fa);
+      mfma_frag<TM, NPAD>(acc, fa, jl);
     } else {
       read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<TM>(acc, fa);
+      mfma_frag<TM, NPAD>(acc, fa, jl);
     }
     const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
     if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
     if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
-    mfma_frag<TM>(acc, fb);
+    mfma_frag<TM, NPAD>(acc, fb, jl);
     cur = nxt;
   }
   lab_stamp<ABL>(p, 2);

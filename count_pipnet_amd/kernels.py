@@ -36,12 +36,13 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant in
     csrc/gemm_f32.hip; alignment is always satisfied by torch allocations)."""
     if k % 16 == 0 and ((k <= 96 and n > 192 and m > 64) or (k % 32 and m > 64)):
-        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0>"
+        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if k % 32:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
     if n <= 384 or k <= 192 or m <= 64:
-        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0>"
-    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0>"
+        npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
+        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
+    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
 
 
 def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
