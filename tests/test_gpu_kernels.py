@@ -20,7 +20,10 @@ def _gemm_tol(a, w):
 
 
 @pytest.mark.parametrize("m,n,k", [(1, 1, 4), (37, 53, 48), (128, 128, 32), (300, 200, 96), (1000, 384, 1536),
-                                   (64, 6144, 2048), (2, 9, 16), (129, 257, 772)])
+                                   (64, 6144, 2048), (2, 9, 16), (129, 257, 772),
+                                   # NPAD tiles (N % 128 != 0, K % 32 == 0): padded 32-column
+                                   # MFMA blocks skipped, wave -> column half flipped per workgroup
+                                   (500, 96, 384), (257, 160, 64), (64, 32, 256), (1000, 100, 512), (3, 4, 32)])
 def test_linear_plain(gpu, m, n, k):
     g = torch.Generator().manual_seed(m * 7 + n * 13 + k)
     a, w = _rand(m, k, gen=g), _rand(n, k, gen=g)
