@@ -358,19 +358,23 @@ PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int
   }
 }
 
-// NPAD: jl (wave-uniform, in an SGPR) = how many of the wave's two 32-column blocks hold
-// columns < N; the MFMAs of a block entirely past N are skipped (N % 128 != 0 grids).
-template <int TM, bool NPAD = false>
-PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f, int jl = 2) {
+// JL = how many of the wave's two 32-column blocks take part (2 everywhere except NPAD
+// waves whose blocks lie past N); a compile-time count, so the MFMA stream stays branch-free.
+template <int TM, int JL = 2>
+PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (!NPAD || j < jl)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < JL; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
 }
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 
 PIPNET_DEV void dma16(const float* src, float* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -464,33 +468,45 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;
   wait_tile(0, issued);
   lab_stamp<ABL>(p, 1);
-  Frag fa, fb;
-  read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const float* buf = smem + cur * G::TILE_FLOATS;
-    if (kt + NS - 1 < nk) {
-      int nb = cur + NS - 1;
-      if (nb >= NS) nb -= NS;
-      stage(kt + NS - 1, nb);
-      issued = kt + NS - 1;
+  // main loop, instantiated per JL (the wave's active 32-column blocks): one wave-uniform
+  // branch here instead of one per MFMA group
+  auto main_loop = [&](auto jlc) {
+    constexpr int JL = decltype(jlc)::value;
+    Frag fa, fb;
+    read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const float* buf = smem + cur * G::TILE_FLOATS;
+      if (kt + NS - 1 < nk) {
+        int nb = cur + NS - 1;
+        if (nb >= NS) nb -= NS;
+        stage(kt + NS - 1, nb);
+        issued = kt + NS - 1;
+      }
+      if constexpr (G::NGROUPS == 4) {
+        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+        mfma_frag<TM, JL>(acc, fa);
+        read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
+        mfma_frag<TM, JL>(acc, fb);
+        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
+        mfma_frag<TM, JL>(acc, fa);
+      } else {
+        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+        mfma_frag<TM, JL>(acc, fa);
+      }
+      const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
+      if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
+      if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
+      mfma_frag<TM, JL>(acc, fb);
+      cur = nxt;
     }
-    if constexpr (G::NGROUPS == 4) {
-      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<TM, NPAD>(acc, fa, jl);
-      read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
-      mfma_frag<TM, NPAD>(acc, fb, jl);
-      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
-      mfma_frag<TM, NPAD>(acc, fa, jl);
-    } else {
-      read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<TM, NPAD>(acc, fa, jl);
-    }
-    const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
-    if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
-    if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
-    mfma_frag<TM, NPAD>(acc, fb, jl);
-    cur = nxt;
+  };
+  if constexpr (NPAD) {
+    if (jl >= 2) main_loop(IntC<2>{});
+    else if (jl == 1) main_loop(IntC<1>{});
+    else main_loop(IntC<0>{});
+  } else {
+    main_loop(IntC<2>{});
   }
   lab_stamp<ABL>(p, 2);
   if (ABL & 2) {
