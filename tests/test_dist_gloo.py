@@ -41,8 +41,17 @@ def _worker(rank, world, port, batch, q):
             own = shard_sizes(batch, world)[rank]
             # per-rank shard path: each rank passes only its own rows
             _, pooled2, out2 = wrapped(xs[start:start + own], inference=True, global_batch=False)
+            # bench.py's call: own shard + every rank's size (no size exchange)
+            _, pooled3, out3 = wrapped(xs[start:start + own], inference=True, global_batch=False,
+                                       sizes=shard_sizes(batch, world))
+            try:
+                wrapped(xs[start:start + own], inference=True, global_batch=False, sizes=[own + 1] * world)
+                bad_sizes_rejected = False
+            except ValueError:
+                bad_sizes_rejected = True
         ok = (torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5)
               and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto.shape[0] == own
+              and torch.equal(pooled, pooled3) and torch.equal(out, out3) and bad_sizes_rejected
               and wrapped.module is net)
         q.put((rank, bool(ok)))
     finally:
