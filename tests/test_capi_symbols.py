@@ -42,3 +42,32 @@ def test_argument_validation_without_gpu():
     # stride 3 is not a ConvNeXt downsample
     assert lib.pipnet_conv2x2_f32(ctypes.c_void_p(16), 1, 4, 4, 32, ctypes.c_void_p(16), None, 8, 3,
                                   ctypes.c_void_p(16), None) == 1
+
+
+def _kernel_symbols():
+    import shutil
+    import subprocess
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    out = subprocess.run([nm, "-C", build.LIB],
+                         capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r"void (pipnet_\w+::\w+<[^>]*>)\(", out))
+
+
+def test_roofline_kernel_names_exist_in_library():
+    """bench.py labels each GEMM launch with kernels.gemm_kernel_name / bf16_conv_kernel_name
+    (the rocprof name it must agree with): every label the ConvNeXt / ResNet / head shapes
+    produce names a kernel instantiated in the library, NPAD tiles included."""
+    from count_pipnet_amd import kernels as K
+    build.build()
+    syms = _kernel_symbols()
+    assert any("gemm_f32_tn_kernel" in s for s in syms)
+    shapes = [(200704, 384, 96, _lib.EPI_BIAS_GELU, 0), (200704, 96, 384, _lib.EPI_RESID, 0),
+              (50176, 768, 192, _lib.EPI_BIAS_GELU, 0), (50176, 192, 768, _lib.EPI_RESID, 0),
+              (46656, 1536, 384, _lib.EPI_BIAS_GELU, 0), (46656, 384, 1536, _lib.EPI_RESID, 0),
+              (43264, 3072, 768, _lib.EPI_BIAS_GELU, 0), (43264, 768, 3072, _lib.EPI_RESID, 0),
+              (50176, 192, 384, _lib.EPI_BIAS, 1), (46656, 384, 768, _lib.EPI_BIAS, 1),
+              (43264, 768, 1536, _lib.EPI_BIAS, 1), (43264, 768, 768, _lib.EPI_NONE, 0),
+              (1024, 16, 192, _lib.EPI_NONE, 0), (46656, 384, 1536, _lib.EPI_RESID_ROWSCALE, 0)]
+    for m, n, k, epi, aload in shapes:
+        name = K.gemm_kernel_name(m, n, k, epi, aload)
+        assert name in syms, (m, n, k, epi, aload, name)
