@@ -104,11 +104,15 @@ def main():
                     help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
     ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
                     help="also time this precision on the same network (reported under alt_precision)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="rehearsal only: torch.distributed backend (default nccl = RCCL on GPUs)")
+    ap.add_argument("--device-index", type=int, default=None,
+                    help="rehearsal only: put every rank on this GPU (multi-rank runs on a 1-GPU box)")
     a = ap.parse_args()
 
     from count_pipnet_amd import build, kernels
     from count_pipnet_amd.dist import ShardedInference, init_from_env
-    rank, world, dev = init_from_env()
+    rank, world, dev = init_from_env(a.dist_backend, a.device_index)
     build.build()
     from count_pipnet_amd.synthetic import synth_images
     net, _ = make_net(dev, precision=a.precision)
@@ -187,7 +191,8 @@ def main():
         "config": {"workload": "PIP-Net ConvNeXt-tiny-26 forward(inference=True), 224x224, 200 classes, fp32 "
                                "(BASELINE configs[1]; configs[3] at N=8)" + (", split-bf16 GEMMs" if split else ""),
                    "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
-                   "parallelism": f"dp{world}", "exchange": "rccl all_gather(logits, pooled)" if world > 1 else None},
+                   "parallelism": f"dp{world}", "exchange": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+                                + " all_gather(logits, pooled)") if world > 1 else None},
         "roofline": roof,
         "model_tflops": gflop_img * a.batch * world / (ms * 1e-3) / 1e3 / world,
         "model_frac_of_f32_peak": gflop_img * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,

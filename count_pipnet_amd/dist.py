@@ -106,19 +106,23 @@ class ShardedInference(nn.Module):
         return proto, pooled, out
 
 
-def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, torch.device]:
+def init_from_env(backend: Optional[str] = None, device_index: Optional[int] = None) -> Tuple[int, int, torch.device]:
     """Initialise torch.distributed from torchrun's env (RANK / WORLD_SIZE / LOCAL_RANK /
-    MASTER_*); backend "nccl" (= RCCL on ROCm) on GPUs, "gloo" on CPU.  Returns
-    (rank, world, device)."""
+    MASTER_*); backend "nccl" (= RCCL on ROCm) on GPUs, "gloo" on CPU.  ``device_index``
+    puts every rank on one GPU (a multi-rank rehearsal on a 1-GPU box, with backend
+    "gloo": RCCL refuses two ranks on one device).  Returns (rank, world, device)."""
     import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if device_index is None else device_index
     use_gpu = torch.cuda.is_available()
     dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         if use_gpu:
             torch.cuda.set_device(local)
-            dist.init_process_group(backend or "nccl", device_id=dev)
+            if (backend or "nccl") == "nccl":
+                dist.init_process_group("nccl", device_id=dev)
+            else:
+                dist.init_process_group(backend)
         else:
             dist.init_process_group(backend or "gloo")
     rank = dist.get_rank() if dist.is_initialized() else 0
