@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpipnet_amd.so")
+LIB_PATH = os.environ.get("PIPNET_AMD_LIB") or os.path.join(_HERE, "libpipnet_amd.so")    # env: A/B builds (tools)
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int

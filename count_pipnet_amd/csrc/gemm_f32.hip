@@ -7,9 +7,12 @@ namespace {
 
 // Raster: consecutive tile ids walk group_m M-tiles before advancing N, sized so the A
 // panels of one group (group_m x 128 rows x K) stay within ~2 MiB of an XCD's 4 MiB L2.
+#ifndef PIPNET_GROUP_BUDGET
+#define PIPNET_GROUP_BUDGET (2.0 * 1024 * 1024)
+#endif
 int choose_group_m(const GemmParams& p) {
   const double panel = 128.0 * p.K * 4.0;
-  int g = (int)(2.0 * 1024 * 1024 / panel);
+  int g = (int)(PIPNET_GROUP_BUDGET / panel);
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 
