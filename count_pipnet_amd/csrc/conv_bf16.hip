@@ -123,7 +123,8 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   // split-bf16 epilogues: only the tiles the automatic choice picks for N < 256 (0 and 4)
 #define PIPNET_S3_CASE(E)                                                                            \
   case E:                                                                                           \
-    if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
+    if (v == 4 && p.N % 128) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2, true>), grid, dim3(256), 0, s, p); \
+    else if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else if (v == 0) hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p); \
     else return PIPNET_ERR_ARG;                                                                     \
     break;

@@ -136,14 +136,21 @@ PIPNET_DEV void read_frag(Frag<C>& f, const bf16* buf, int wm, int wn, int lr, i
   }
 }
 
-template <class C>
+// JL = the wave's active 32-column blocks (TN except NPAD waves whose blocks lie past N),
+// a compile-time count so the MFMA stream stays branch-free.
+template <class C, int JL = C::TN>
 PIPNET_DEV void mfma_frag(Acc<C>& acc, const Frag<C>& f) {
 #pragma unroll
   for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j)
+    for (int j = 0; j < JL; ++j)
       acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
 }
+
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
 
 PIPNET_DEV void dma16(const void* src, bf16* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
@@ -289,7 +296,9 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
 // fragments software-pipelined over the tile's chunk groups (group q of half-wave h = chunk
 // h*NGROUPS + q = k 8(h*NGROUPS + q) .. +7 of the tile).  NS = 2 waits with vmcnt(0); NS >= 3
 // with a counted vmcnt and a raw s_barrier so younger tiles' DMA spans the barrier.
-template <class C, int EPI, int ALOAD, int MINB>
+// NPAD (N % BNT != 0, two wave columns): MFMA blocks of columns >= N are skipped and the
+// wave -> column-half map flips with the workgroup parity (as the fp32 GEMM's NPAD tiles).
+template <class C, int EPI, int ALOAD, int MINB, bool NPAD = false>
 __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams p) {
   constexpr int NS = C::NS, BK = C::BK;
   constexpr int NWAVES = C::NWAVES;
@@ -300,11 +309,14 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid / C::WGN, wn = wid % C::WGN;
+  static_assert(!NPAD || C::WGN == 2, "NPAD flips between two wave columns");
+  const int wm = wid / C::WGN, wn = NPAD ? ((wid % C::WGN) ^ (int)(blockIdx.x & 1)) : wid % C::WGN;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
   tile_coords(p, C::BMT, C::BNT, m0, n0);
   const int nk = p.K / BK;
+  const int jl = NPAD ? __builtin_amdgcn_readfirstlane(min(C::TN, max(0, (p.N - n0 - wn * 32 * C::TN + 31) >> 5)))
+                      : C::TN;
 
   const int drow = lane / C::CHUNKS;
   ARow arow[C::A_DMA];
@@ -354,33 +366,44 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
   int issued = -1;
   for (int s0 = 0; s0 < NS - 1 && s0 < nk; ++s0) stage(s0, s0), issued = s0;
   wait_tile(0, issued);
-  Frag<C> fa, fb;
-  read_frag<C>(fa, smem, wm, wn, lr, lh, 0);
-  int cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const bf16* buf = smem + cur * C::TILE_ELEMS;
-    if (kt + NS - 1 < nk) {
-      int nb = cur + NS - 1;
-      if (nb >= NS) nb -= NS;
-      stage(kt + NS - 1, nb);
-      issued = kt + NS - 1;
+  auto main_loop = [&](auto jlc) {
+    constexpr int JL = decltype(jlc)::value;
+    Frag<C> fa, fb;
+    read_frag<C>(fa, smem, wm, wn, lr, lh, 0);
+    int cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bf16* buf = smem + cur * C::TILE_ELEMS;
+      if (kt + NS - 1 < nk) {
+        int nb = cur + NS - 1;
+        if (nb >= NS) nb -= NS;
+        stage(kt + NS - 1, nb);
+        issued = kt + NS - 1;
+      }
+      if constexpr (C::NGROUPS == 4) {
+        read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
+        mfma_frag<C, JL>(acc, fa);
+        read_frag<C>(fa, buf, wm, wn, lr, lh, 2);
+        mfma_frag<C, JL>(acc, fb);
+        read_frag<C>(fb, buf, wm, wn, lr, lh, 3);
+        mfma_frag<C, JL>(acc, fa);
+      } else {
+        read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
+        mfma_frag<C, JL>(acc, fa);
+      }
+      const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
+      wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);     // tile kt+1 landed, tile kt read
+      if (kt + 1 < nk) read_frag<C>(fa, smem + nxt * C::TILE_ELEMS, wm, wn, lr, lh, 0);
+      mfma_frag<C, JL>(acc, fb);
+      cur = nxt;
     }
-    if constexpr (C::NGROUPS == 4) {
-      read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<C>(acc, fa);
-      read_frag<C>(fa, buf, wm, wn, lr, lh, 2);
-      mfma_frag<C>(acc, fb);
-      read_frag<C>(fb, buf, wm, wn, lr, lh, 3);
-      mfma_frag<C>(acc, fa);
-    } else {
-      read_frag<C>(fb, buf, wm, wn, lr, lh, 1);
-      mfma_frag<C>(acc, fa);
-    }
-    const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
-    wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);     // tile kt+1 landed, tile kt read
-    if (kt + 1 < nk) read_frag<C>(fa, smem + nxt * C::TILE_ELEMS, wm, wn, lr, lh, 0);
-    mfma_frag<C>(acc, fb);
-    cur = nxt;
+  };
+  if constexpr (NPAD) {
+    static_assert(C::TN == 2, "NPAD dispatch covers TN = 2");
+    if (jl >= 2) main_loop(IntC<2>{});
+    else if (jl == 1) main_loop(IntC<1>{});
+    else main_loop(IntC<0>{});
+  } else {
+    main_loop(IntC<C::TN>{});
   }
   epilogue<EPI, C>(p, acc, reinterpret_cast<float*>(smem), m0, n0, wm, wn, lane, wid);
 }

@@ -225,7 +225,8 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 7:
         return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 3>"
     cfg, minb = _BF16_CFG[t]
-    return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}>"
+    npad = "true" if s3 and t == 4 and n % 128 else "false"     # padded-column MFMA blocks skipped
+    return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}, {npad}>"
 
 
 def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:

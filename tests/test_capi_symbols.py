@@ -50,7 +50,7 @@ def _kernel_symbols():
     nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
     out = subprocess.run([nm, "-C", build.LIB],
                          capture_output=True, text=True, check=True).stdout
-    return set(re.findall(r"void (pipnet_\w+::\w+<[^>]*>)\(", out))
+    return set(re.findall(r"void (pipnet_\w+::\w+<.*>)\(", out))     # greedy: nested Cfg<...>
 
 
 def test_roofline_kernel_names_exist_in_library():
@@ -71,3 +71,10 @@ def test_roofline_kernel_names_exist_in_library():
     for m, n, k, epi, aload in shapes:
         name = K.gemm_kernel_name(m, n, k, epi, aload)
         assert name in syms, (m, n, k, epi, aload, name)
+    # split-bf16 ConvNeXt GEMMs (stage-1/2 fc1 / fc2 incl. the N = 96 padded-column tile) and
+    # ResNet bf16 convs
+    for m, n, epi, s3 in [(200704, 96, _lib.EPI_F32_RESID, True), (200704, 384, _lib.EPI_S3_GELU, True),
+                          (50176, 192, _lib.EPI_F32_RESID, True), (401408, 64, _lib.EPI_BIAS_RELU, False),
+                          (100352, 128, _lib.EPI_BIAS_RELU, False)]:
+        name = K.bf16_conv_kernel_name(m, n, epi, 0, s3=s3)
+        assert name in syms, (m, n, epi, s3, name)
