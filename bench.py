@@ -71,25 +71,62 @@ class GemmTimer:
         return agg
 
 
-def cpu_baseline(batch=4, min_seconds=10.0):
-    """The oracle (pure-torch CPU restatement of the reference forward) on the host cores."""
+def measured_traffic(dom):
+    """HBM bytes per launch of the dominant kernel from the committed PMC measurement
+    (tools/pmc.sh -> tools/pmc_summary.py -> profiles/traffic_latest.json), used only when it
+    was measured on this exact kernel: same kernel name AND same sha256 of the kernel
+    family's sources.  Otherwise (kernel changed since the PMC pass) traffic is null."""
+    from count_pipnet_amd.build import kernel_source_digest
+    path = os.path.join(REPO, "profiles", "traffic_latest.json")
+    if not os.path.exists(path):
+        return None, "no PMC measurement"
+    with open(path) as f:
+        tr = json.load(f)
+    if tr.get("kernel_key") != dom:
+        return None, f"PMC measurement is of another kernel ({tr.get('kernel_key')})"
+    if not tr.get("source_digest") or tr["source_digest"] != kernel_source_digest(dom):
+        return None, "PMC measurement predates the current kernel sources (digest mismatch)"
+    return tr.get("hbm_bytes_per_launch"), "profiles/traffic_latest.json (" + tr.get("method", "") + ")"
+
+
+def _cpu_model():
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(batch=64, repeats=3):
+    """The oracle (pure-torch CPU restatement of the reference forward, parity-pinned to the
+    reference's goldens) on the host cores, by SURVEY.md 8(d) / BASELINE.md's protocol:
+    the same 64-image 224x224 batch as the GPU step, 1 warm-up forward, then the median of
+    3 timed forwards.  Reports nproc, the lscpu model name and torch's thread count."""
+    import statistics
     from oracle import ref_cpu
     from count_pipnet_amd.synthetic import synth_images
     net, args = make_net(torch.device("cpu"))
     sd = {k: v for k, v in net.state_dict().items()}
     xs = synth_images(batch, 224, seed=1)
+    times = []
     with torch.no_grad():
-        ref_cpu.pipnet_forward(xs[:1], sd, args, inference=True)       # warm-up
-        n, t0 = 0, time.perf_counter()
-        while True:
+        ref_cpu.pipnet_forward(xs, sd, args, inference=True)       # warm-up
+        for _ in range(repeats):
+            t0 = time.perf_counter()
             ref_cpu.pipnet_forward(xs, sd, args, inference=True)
-            n += batch
-            el = time.perf_counter() - t0
-            if el >= min_seconds:
-                break
-    return {"value": n / el, "unit": "images/sec", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} images (batches of {batch}, 224x224, ConvNeXt-tiny-26 PIP-Net fp32) in {el:.1f} s, "
-                      f"oracle/ref_cpu.py pipnet_forward on {torch.get_num_threads()} threads"}
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    threads = torch.get_num_threads()
+    return {"value": batch / med, "unit": "images/sec", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "torch_threads": threads,
+            "batch_seconds": times,
+            "sample": f"one {batch}-image 224x224 batch (ConvNeXt-tiny-26 PIP-Net fp32, inference=True), "
+                      f"1 warm-up + median of {repeats} = {med:.2f} s/batch; oracle/ref_cpu.py pipnet_forward "
+                      f"on {threads} torch threads; nproc={os.cpu_count()}, CPU: {_cpu_model()}"}
 
 
 def main():
@@ -99,7 +136,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
                     help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
     ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
@@ -213,14 +249,9 @@ def main():
             "accuracy": "fp32 inputs/outputs and accumulation; products of hi+lo bf16 splits (~1e-5 relative "
                         "per product); parity vs the reference goldens at the north-star 1e-3 "
                         "(tests/test_gpu_parity.py::test_hip_bf16x3_*)" if a.alt_precision == "bf16x3" else "exact"}
-    traffic_path = os.path.join(REPO, "profiles", "traffic_latest.json")
-    if os.path.exists(traffic_path):
-        with open(traffic_path) as f:
-            tr = json.load(f)
-        if tr.get("kernel_key") == dom:
-            result["roofline"]["traffic"] = tr.get("hbm_bytes_per_launch")
+    result["roofline"]["traffic"], result["roofline"]["traffic_source"] = measured_traffic(dom)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(min_seconds=a.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -24,6 +24,7 @@ F64 = ctypes.c_double
 SIGNATURES = {
     "pipnet_amd_abi_version": [],
     "pipnet_amd_status_string": [I32],
+    "pipnet_amd_source_digest": [],
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],
     "pipnet_linear_splitk_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, I32, P, P],
@@ -82,7 +83,8 @@ SIGNATURES = {
     "pipnet_head_bwd_f32": [P, P, I32, I32, I32, P, P, I32, F32, F32, F32, P, P, P, P],
 }
 _RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64}
-_RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, **_RESTYPE_EXTRA}
+_RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, "pipnet_amd_source_digest": ctypes.c_char_p,
+            **_RESTYPE_EXTRA}
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_RESID_RELU = 0, 1, 2, 3, 4, 5, 6
 EPI_RESID_ROWSCALE = 7
@@ -111,8 +113,22 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)          # AttributeError = missing export = loud failure
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, ctypes.c_int)
+    _check_provenance(lib)
     _lib = lib
     return lib
+
+
+def _check_provenance(lib) -> None:
+    """The library must have been compiled from the sources of this tree (sha256 compiled
+    in by build.py).  ``PIPNET_AMD_ALLOW_STALE=1`` is the explicit A/B escape hatch (e.g. an
+    experimental build loaded through ``PIPNET_AMD_LIB``)."""
+    from .build import source_digest
+    built = lib.pipnet_amd_source_digest().decode()
+    here = source_digest()
+    if built != here and os.environ.get("PIPNET_AMD_ALLOW_STALE") != "1":
+        raise PipnetLibraryError(
+            f"{LIB_PATH} was built from other sources (digest {built[:16]}..., tree {here[:16]}...): "
+            "rebuild with `python count_pipnet_amd/build.py` (or set PIPNET_AMD_ALLOW_STALE=1 for an A/B run)")
 
 
 def check(status: int, what: str) -> None:

@@ -592,6 +592,14 @@ extern "C" int pipnet_count_encode_f32(const float* x, int B, int P, int C, int 
 
 extern "C" int pipnet_amd_abi_version(void) { return 1; }
 
+// sha256 over the library's sources (csrc/*.hip, csrc/*.hpp, include/*.h), computed by
+// count_pipnet_amd/build.py and passed on the hipcc line; _lib.load() compares it with the
+// tree it runs from, so a shipped binary built from other sources fails loudly.
+#ifndef PIPNET_SRC_DIGEST
+#define PIPNET_SRC_DIGEST "unknown"
+#endif
+extern "C" const char* pipnet_amd_source_digest(void) { return PIPNET_SRC_DIGEST; }
+
 extern "C" const char* pipnet_amd_status_string(int status) {
   switch (status) {
     case PIPNET_OK: return "ok";

@@ -9,8 +9,12 @@ gathers all three outputs back to GPU 0.  Here:
   * the global batch is split exactly like ``DataParallel.scatter`` (``torch.chunk`` along
     dim 0, so shard sizes and order match), or each rank passes its own shard;
   * the only exchange is one all-gather of ``pooled`` [B/N, P] and ``out`` [B/N, K]
-    (and optionally ``proto_features``) over RCCL/xGMI -- no reduction is needed because
-    images are independent.
+    over RCCL/xGMI -- no reduction is needed because images are independent (SURVEY.md 8e);
+  * ``proto_features`` is gathered too when the caller uses DataParallel's call pattern
+    (the full batch on every rank), because DataParallel gathers all three outputs and
+    callers index ``proto_features[i]`` across the batch (util/vis_pipnet.py:25).  Callers
+    that pass their own shard (``global_batch=False``, e.g. bench.py) get their shard's map
+    unless they ask for the gather.
 
 ``ShardedInference`` keeps DataParallel's ``.module`` attribute, so callers written for
 the reference (``net.module._classification``, ``net.module._num_classes`` in
@@ -59,7 +63,7 @@ def all_gather_rows(x: Tensor, sizes: List[int], group=None) -> Tensor:
 class ShardedInference(nn.Module):
     """Data-parallel inference wrapper (DataParallel semantics, one process per GPU)."""
 
-    def __init__(self, module: nn.Module, process_group=None, gather_proto: bool = False):
+    def __init__(self, module: nn.Module, process_group=None, gather_proto: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.process_group = process_group
@@ -78,8 +82,10 @@ class ShardedInference(nn.Module):
         """``global_batch=True``: ``xs`` is the full batch on every rank (DataParallel call
         pattern) and this rank takes its ``torch.chunk`` shard.  ``False``: ``xs`` is this
         rank's own shard (pass ``sizes`` -- every rank's shard size -- to skip the size
-        exchange and its host sync).  Returns (proto_features of this rank's shard -- or of the whole
-        batch with ``gather_proto`` --, pooled [B, P], out [B, K]) in global batch order."""
+        exchange and its host sync).  Returns (proto_features, pooled [B, P], out [B, K]) in global
+        batch order; proto_features covers the whole batch when ``gather_proto`` is True, or
+        when it is None (the default) and ``global_batch`` is True -- DataParallel's outputs --,
+        and this rank's shard otherwise."""
         world, rank = self.world, self.rank
         if global_batch:
             sizes = shard_sizes(xs.shape[0], world)
@@ -101,9 +107,20 @@ class ShardedInference(nn.Module):
         proto, pooled, out = self.module(local, inference=inference)
         pooled = all_gather_rows(pooled, sizes, self.process_group)
         out = all_gather_rows(out, sizes, self.process_group)
-        if self.gather_proto:
-            proto = all_gather_rows(proto.contiguous(), sizes, self.process_group)
+        gather_proto = global_batch if self.gather_proto is None else self.gather_proto
+        if gather_proto and world > 1:
+            proto = gather_proto_features(proto, sizes, self.process_group)
         return proto, pooled, out
+
+
+def gather_proto_features(proto: Tensor, sizes: List[int], group=None) -> Tensor:
+    """All-gather a [b, P, h, w] prototype map.  The HIP path returns it as a view of NHWC
+    storage (channels_last strides); it is exchanged in that storage order (no transpose
+    on either side) and handed back with the same strides."""
+    if proto.dim() == 4 and proto.permute(0, 2, 3, 1).is_contiguous():
+        g = all_gather_rows(proto.permute(0, 2, 3, 1), sizes, group)
+        return g.permute(0, 3, 1, 2)
+    return all_gather_rows(proto.contiguous(), sizes, group)
 
 
 def init_from_env(backend: Optional[str] = None, device_index: Optional[int] = None) -> Tuple[int, int, torch.device]:

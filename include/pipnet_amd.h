@@ -48,6 +48,8 @@ extern "C" {
 
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
+/* sha256 (hex) of the sources this library was compiled from (build provenance). */
+const char* pipnet_amd_source_digest(void);
 
 /* Dense fp32 linear / 1x1 conv on MFMA (v_mfma_f32_32x32x2_f32, exact fp32):
  *   C[M,N] (ldc) = epi( A[M,K] (lda) * W[N,K]^T )

@@ -29,6 +29,28 @@ def test_library_loads_and_exports_all_symbols():
     assert lib.pipnet_amd_status_string(1).decode().startswith("invalid argument")
 
 
+def test_library_digest_matches_sources(tmp_path, monkeypatch):
+    """Build provenance is a content digest compiled into the library, not a file mtime:
+    the loaded library's digest equals the tree's, and a changed source is seen as stale
+    whatever the mtimes say."""
+    build.build()
+    lib = _lib.load()
+    assert lib.pipnet_amd_source_digest().decode() == build.source_digest()
+    assert not build.is_stale()
+    hdr = tmp_path / "extra.h"
+    hdr.write_text("/* changed */\n")
+    monkeypatch.setattr(build, "_deps", lambda orig=build._deps: orig() + [str(hdr)])
+    assert build.is_stale()
+    monkeypatch.setattr(_lib, "_lib", None)
+    try:
+        _lib.load()
+        raise AssertionError("a library built from other sources loaded")
+    except _lib.PipnetLibraryError as e:
+        assert "other sources" in str(e)
+    monkeypatch.setenv("PIPNET_AMD_ALLOW_STALE", "1")
+    assert _lib.load() is not None
+
+
 def test_argument_validation_without_gpu():
     """Bad shapes are rejected before any HIP call (status PIPNET_ERR_ARG, no launch)."""
     lib = _lib.load()

@@ -1,6 +1,7 @@
 """Multi-process data-parallel inference (count_pipnet_amd.dist) on CPU with gloo,
 world_size 2: DataParallel-style sharding (torch.chunk order, uneven shards) and the
-all-gather of pooled / logits reproduce the single-process full-batch forward."""
+all-gather of proto / pooled / logits reproduce the single-process full-batch forward.
+The HIP path under the same wrapper is tests/test_gpu_dist.py."""
 import os
 import socket
 
@@ -36,11 +37,11 @@ def _worker(rank, world, port, batch, q):
         wrapped = ShardedInference(net)
         with torch.no_grad(), torch_backend():
             proto, pooled, out = wrapped(xs, inference=True)
-            _, r_pooled, r_out = net(xs, inference=True)
+            r_proto, r_pooled, r_out = net(xs, inference=True)
             start = sum(shard_sizes(batch, world)[:rank])
             own = shard_sizes(batch, world)[rank]
             # per-rank shard path: each rank passes only its own rows
-            _, pooled2, out2 = wrapped(xs[start:start + own], inference=True, global_batch=False)
+            proto2, pooled2, out2 = wrapped(xs[start:start + own], inference=True, global_batch=False)
             # bench.py's call: own shard + every rank's size (no size exchange)
             _, pooled3, out3 = wrapped(xs[start:start + own], inference=True, global_batch=False,
                                        sizes=shard_sizes(batch, world))
@@ -50,7 +51,9 @@ def _worker(rank, world, port, batch, q):
             except ValueError:
                 bad_sizes_rejected = True
         ok = (torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5)
-              and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto.shape[0] == own
+              and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto2.shape[0] == own
+              # DataParallel call pattern: all three outputs cover the whole batch
+              and proto.shape == r_proto.shape and torch.allclose(proto, r_proto, atol=1e-6)
               and torch.equal(pooled, pooled3) and torch.equal(out, out3) and bad_sizes_rejected
               and wrapped.module is net)
         q.put((rank, bool(ok)))

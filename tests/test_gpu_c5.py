@@ -1,0 +1,110 @@
+"""BASELINE C5 at its real per-GPU size: CountPIPNet bilinear.yaml, 64 images of 128x128 per
+GPU (bs=256 over 4 GPUs), 2048 prototypes, 16x16 grid (/root/reference/pipnet/count_pipnet.py:70-110,
+GumbelSoftmax count_pipnet_utils.py:23-38, BilinearIntermediate :323-385).
+
+The golden covers bs=2; here the Gumbel / count head runs at its real grid (64 x 256 pixels x
+2048 channels) with an injected Exp(1) draw, and these size-independent properties hold:
+
+* one-hot rows: every pixel's proto column has exactly one nonzero, equal to 1 within 1 ulp
+  (``y_hard - y_soft + y_soft``) and at the argmax of logits - log(E) (checked for four images
+  against the oracle, whole maps);
+* counts = histogram: inference counts = clamp(round(sum over pixels), 0, 3), raw counts =
+  the pixel sums, and both equal the per-image histogram of the one-hot argmax positions;
+* logits = NonNegLinear(BilinearIntermediate(counts)) with the module's own weights, in fp64
+  on the host (the reference's arithmetic restated by the oracle), at 1e-3 of scale;
+* batch invariance: images 5..7 run alone give bit-identical proto / counts / logits;
+* four images end to end against the oracle with the same noise: the one-hot position of
+  every pixel whose Gumbel top-2 gap is >= 1e-3, and for images without such a near-tie the
+  counts exactly and the logits at 1e-3.
+"""
+import numpy as np
+import pytest
+import torch
+
+from count_pipnet_amd.synthetic import synth_exponential, synth_images
+from golden_util import golden_args, load_golden
+from model_util import build_model
+from oracle import ref_cpu
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-3
+B, SIZE, P, GRID = 64, 128, 2048, 16
+NO = 4      # images checked against the oracle
+
+
+@pytest.fixture(scope="module")
+def c5(gpu):
+    meta, _ = load_golden("c5_count_bilinear_2048")
+    net = build_model(meta).to(gpu)
+    xs = synth_images(B, SIZE, seed=55)
+    noise = synth_exponential((B, P, GRID, GRID), seed=56)
+    net._add_on[-1].exp_noise = noise.to(gpu)
+    with torch.no_grad():
+        proto, counts, out = net(xs.to(gpu), inference=True)
+        _, raw, out_raw = net(xs.to(gpu), inference=False)
+        net._add_on[-1].exp_noise = noise[5:8].to(gpu)
+        proto3, counts3, out3 = net(xs[5:8].to(gpu), inference=True)
+    torch.cuda.synchronize()
+    return dict(meta=meta, net=net, xs=xs, noise=noise, proto=proto, counts=counts, out=out, raw=raw,
+                out_raw=out_raw, proto3=proto3, counts3=counts3, out3=out3)
+
+
+def test_c5_shapes_and_one_hot_rows(c5):
+    proto = c5["proto"]
+    assert proto.shape == (B, P, GRID, GRID) and c5["counts"].shape == (B, P) and c5["out"].shape == (B, 9)
+    nnz = (proto != 0).sum(dim=1)
+    assert torch.equal(nnz, torch.ones_like(nnz)), "every pixel holds exactly one nonzero"
+    top = proto.amax(dim=1)
+    assert (top - 1.0).abs().max().item() <= 2 ** -23
+
+
+def test_c5_counts_are_histograms(c5):
+    proto, counts, raw = c5["proto"], c5["counts"], c5["raw"]
+    idx = proto.argmax(dim=1).flatten(1)                                       # [B, 256]
+    hist = torch.zeros(B, P, device=proto.device).scatter_add_(1, idx, torch.ones_like(idx, dtype=torch.float32))
+    assert torch.allclose(raw, hist, atol=256 * 2 ** -23)                     # raw counts = pixel sums
+    assert torch.equal(counts, hist.round().clamp(0, 3))                       # STE_Round + ClampSTE
+    assert torch.equal(counts, raw.round().clamp(0, 3))
+
+
+def test_c5_logits_from_counts(c5):
+    """out = relu(W_cls) . (W(e) * V(e)), e = embed(counts): the intermediate and classifier
+    recomputed in fp64 from the HIP counts with the module's own parameters."""
+    net = c5["net"]
+    sd = {k: v.detach().cpu().double() for k, v in net.state_dict().items()}
+    for counts, out in ((c5["counts"], c5["out"]), (c5["raw"], c5["out_raw"])):
+        c = counts.cpu().double()
+        e = c @ sd["_intermediate.embed.weight"].t()
+        inter = (e @ sd["_intermediate.W.weight"].t()) * (e @ sd["_intermediate.V.weight"].t())
+        ref = inter @ sd["_classification.weight"].clamp(min=0).t()
+        if "_classification.bias" in sd:
+            ref = ref + sd["_classification.bias"]
+        scale = ref.abs().clamp(min=1.0)
+        assert ((out.cpu().double() - ref).abs() / scale).max().item() <= TOL
+
+
+def test_c5_batch_invariance(c5):
+    assert torch.equal(c5["proto"][5:8], c5["proto3"])
+    assert torch.equal(c5["counts"][5:8], c5["counts3"])
+    assert torch.equal(c5["out"][5:8], c5["out3"])
+
+
+def test_c5_images_vs_oracle(c5):
+    net, meta = c5["net"], c5["meta"]
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    with torch.no_grad():
+        r_proto, r_counts, r_out = ref_cpu.count_pipnet_forward(c5["xs"][:NO], sd, golden_args(meta), inference=True,
+                                                                 exp_noise=c5["noise"][:NO])
+        # images with a Gumbel near-tie (top-2 gap < 1e-3 somewhere) may pick the other channel
+        feats = torch.nn.functional.conv2d(ref_cpu.backbone(c5["xs"][:NO], sd, golden_args(meta)),
+                                           sd["_add_on.0.weight"], sd["_add_on.0.bias"])
+        top2 = (feats - c5["noise"][:NO].log()).topk(2, dim=1).values
+        decisive = (top2[:, 0] - top2[:, 1]) >= TOL                           # [NO, 16, 16]
+        ok = decisive.flatten(1).all(dim=1).numpy()
+    proto, counts, out = c5["proto"][:NO].cpu(), c5["counts"][:NO].cpu(), c5["out"][:NO].cpu()
+    # the one-hot position of every decisive pixel of every image
+    assert torch.equal(proto.argmax(dim=1)[decisive], r_proto.argmax(dim=1)[decisive])
+    assert ok.any(), "every oracle image holds a Gumbel near-tie; pick other seeds"
+    for i in np.nonzero(ok)[0]:
+        assert torch.equal(counts[i], r_counts[i])
+        assert ((out[i] - r_out[i]).abs() / r_out[i].abs().clamp(min=1)).max().item() <= TOL

@@ -10,6 +10,8 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from count_pipnet_amd.build import kernel_source_digest  # noqa: E402
 
 
 def load(pass_dir):
@@ -58,6 +60,7 @@ if gemms:
     tr = dict(kernel_key=dom, hbm_bytes_per_launch=gemms[dom]["hbm_bytes"],
               hbm_read_bytes_per_launch=gemms[dom]["hbm_read_bytes"],
               hbm_write_bytes_per_launch=gemms[dom]["hbm_write_bytes"], avg_us=gemms[dom]["avg_us"],
+              source_digest=kernel_source_digest(dom),
               method="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh); "
                      "FETCH_SIZE x2 (gfx950 wide-read undercount), KB -> bytes")
     json.dump(tr, open(os.path.join(d, "traffic_latest.json"), "w"), indent=1)
