@@ -19,7 +19,7 @@ for s in $STEPS; do
     dwlab) timeout -k 10 300 python tools/dw_lab.py > gpurun_out/dw_lab.log 2>&1; stop_if_fatal $? dwlab; grep -v "^\[\|amdgpu.ids" gpurun_out/dw_lab.log | tail -8 ;;
     cfgs)  timeout -k 10 600 python tools/bench_configs.py > gpurun_out/bench_configs.log 2>&1; stop_if_fatal $? cfgs; grep "^{" gpurun_out/bench_configs.log ;;
     convbf) timeout -k 10 300 python tools/conv_bf16_bench.py > gpurun_out/conv_bf16.log 2>&1; stop_if_fatal $? convbf; grep -v "^\[" gpurun_out/conv_bf16.log | tail -20 ;;
-    profc3) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/profc3" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/bench_configs.py" --only c3 --steps 5 > "$GRAFT_REPO_ROOT/gpurun_out/profc3.log" 2>&1); stop_if_fatal $? profc3 ;;
+    profcfg) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_${CFG}" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/bench_configs.py" --only ${CFG} --steps 5 > "$GRAFT_REPO_ROOT/gpurun_out/prof_${CFG}.log" 2>&1); stop_if_fatal $? profcfg ;;
     pmcg)  timeout -k 10 900 bash tools/pmc_generic.sh > gpurun_out/pmcg.log 2>&1; stop_if_fatal $? pmcg; tail -60 gpurun_out/pmcg.log ;;
     gemm)  timeout -k 10 300 python tools/gemm_bench.py > gpurun_out/gemm_bench.log 2>&1; stop_if_fatal $? gemm; grep -v "^\[" gpurun_out/gemm_bench.log | tail -20 ;;
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; stop_if_fatal $? bench; tail -3 gpurun_out/bench.log ;;
