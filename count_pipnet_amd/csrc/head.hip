@@ -169,8 +169,11 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
 }
 
 // ---------------------------------------------------------------------------------------
-// NonNegLinear: grid (image, class block of 16); x' staged in LDS; each wave computes 4
-// classes at once (4 independent dot products in flight, float4 W reads).
+// NonNegLinear: grid (image, class block of 16).  Every thread owns a float4 slice of the
+// feature dimension (c = 4*tid, 4*tid + 1024, ...) and keeps 16 class partials, so one pass
+// over x issues 16 independent float4 W loads per slice (C5: D = 6144, K = 9 -> 6 slices x 9
+// loads in flight per thread; C2: D = 768, K = 200 -> 13 blocks per image).  Partials are
+// reduced wave-wise then across the 4 waves in a fixed order (batch-invariant).
 // ---------------------------------------------------------------------------------------
 constexpr int NN_CLS_PER_BLOCK = 16;
 
@@ -180,41 +183,56 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
                                                                      int apply_thresh, float thresh,
                                                                      float* __restrict__ x_out,
                                                                      float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float xs[];
-  const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
-    float v = x[(int64_t)b * D + c];
-    if (apply_thresh && v < thresh) v = 0.f;
-    xs[c] = v;
-    if (x_out && blockIdx.y == 0) x_out[(int64_t)b * D + c] = v;
-  }
-  __syncthreads();
+  __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
+  const int b = blockIdx.x, k0 = blockIdx.y * NN_CLS_PER_BLOCK;
+  const int nk = K - k0 < NN_CLS_PER_BLOCK ? K - k0 : NN_CLS_PER_BLOCK;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int k0 = blockIdx.y * NN_CLS_PER_BLOCK + wv * 4;
-  const bool vec = (D & 3) == 0;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  const float* xr = x + (int64_t)b * D;
+  const float* w0 = W + (int64_t)k0 * D;
+  float s[NN_CLS_PER_BLOCK];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = k0 + j;
-    if (k >= K) break;
-    const float* wr = W + (int64_t)k * D;
-    if (vec) {
-      for (int c = 4 * lane; c < D; c += 256) {
-        const f32x4 wv4 = ld4(wr + c), xv = ld4(xs + c);
-        s[j] = fmaf(xv[0], fmaxf(wv4[0], 0.f), s[j]);
-        s[j] = fmaf(xv[1], fmaxf(wv4[1], 0.f), s[j]);
-        s[j] = fmaf(xv[2], fmaxf(wv4[2], 0.f), s[j]);
-        s[j] = fmaf(xv[3], fmaxf(wv4[3], 0.f), s[j]);
+  for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) s[j] = 0.f;
+  if ((D & 3) == 0) {
+    for (int c = 4 * threadIdx.x; c < D; c += 4 * HEAD_THREADS) {
+      f32x4 xv = ld4(xr + c);
+      if (apply_thresh) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xv[e] = xv[e] < thresh ? 0.f : xv[e];
       }
-    } else {
-      for (int c = lane; c < D; c += 64) s[j] = fmaf(xs[c], fmaxf(wr[c], 0.f), s[j]);
+      if (x_out && blockIdx.y == 0) st4(x_out + (int64_t)b * D + c, xv);
+#pragma unroll
+      for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
+        if (j < nk) {
+          const f32x4 w = ld4(w0 + (int64_t)j * D + c);
+          s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
+          s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
+          s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
+          s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
+        }
+      }
+    }
+  } else {
+    for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
+      float xv = xr[c];
+      if (apply_thresh && xv < thresh) xv = 0.f;
+      if (x_out && blockIdx.y == 0) x_out[(int64_t)b * D + c] = xv;
+#pragma unroll
+      for (int j = 0; j < NN_CLS_PER_BLOCK; ++j)
+        if (j < nk) s[j] = fmaf(xv, fmaxf(w0[(int64_t)j * D + c], 0.f), s[j]);
     }
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int k = k0 + j;
+  for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
     const float t = wave_sum(s[j]);
-    if (lane == 0 && k < K) out[(int64_t)b * K + k] = t + (bias ? bias[k] : 0.f);
+    if (lane == 0) red[wv][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < nk) {
+    const int k = k0 + threadIdx.x;
+    float t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < HEAD_THREADS / 64; ++w) t += red[w][threadIdx.x];
+    out[(int64_t)b * K + k] = t + (bias ? bias[k] : 0.f);
   }
 }
 
@@ -262,7 +280,9 @@ PIPNET_DEV float exp1_from_bits(uint32_t w) {
 // softmax((x - log E) / tau) written for every channel, and the per-prototype spatial sums
 // (the raw counts, count_pipnet.py:88) reduced per workgroup in LDS, one float atomic per
 // (workgroup, channel) into `sums`.
-template <int NJ, bool SOFT = false>
+constexpr int CG_PIX_PER_BLOCK = 16;        // 4 pixels per wave: C5 (64 x 256 px) -> 1024 workgroups
+
+template <int NJ, bool SOFT = false, bool NOISE = false>   // NOISE: injected Exp(1) draw, else Philox
 __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float* __restrict__ logits, int HW, int P,
                                                                     float inv_tau,
                                                                     const float* __restrict__ exp_noise,
@@ -275,7 +295,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
   if (seed_dev) seed = *seed_dev;            // graph-replay form: the seed lives in device memory
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
-  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  const int pix0 = blockIdx.x * CG_PIX_PER_BLOCK;
   float racc[SOFT ? NJ4 : 1][4];
   if constexpr (SOFT) {
 #pragma unroll
@@ -283,20 +303,38 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
 #pragma unroll
       for (int e = 0; e < 4; ++e) racc[j][e] = 0.f;
   }
-  for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
+  // the wave's pixels pix0 + wv, + 4, ...: the next pixel's logits are loaded before the
+  // current pixel's noise / argmax / exp work, so HBM reads overlap the VALU part
+  f32x4 xn[NJ4];
+  auto load_px = [&](int pix) {
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+#pragma unroll
+    for (int j = 0; j < NJ4; ++j) {
+      const int c = 4 * lane + 256 * j;
+      if (c < P) xn[j] = ld4(logits + base + c);
+    }
+  };
+  if (pix0 + wv < HW) load_px(pix0 + wv);
+  for (int pi = wv; pi < CG_PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
     const int pix = pix0 + pi;
     if (pix >= HW) break;
     const int64_t base = ((int64_t)b * HW + pix) * P;
-    float z[NJ4][4];
-    float m = -INFINITY;
+    f32x4 xc[NJ4];
+#pragma unroll
+    for (int j = 0; j < NJ4; ++j) xc[j] = xn[j];
+    if (pi + HEAD_THREADS / 64 < CG_PIX_PER_BLOCK && pix + HEAD_THREADS / 64 < HW) load_px(pix + HEAD_THREADS / 64);
+    // hard (eval) head: one pass per lane with a running (max, first argmax, sum of exp(z - max))
+    // -- no per-element z kept, so the kernel stays at 4 waves per SIMD; the lanes' sums are
+    // rescaled to the wave max before the wave sum.  SOFT keeps z for the normalised write.
+    float z[SOFT ? NJ4 : 1][4];
+    float m = -INFINITY, ls = 0.f;
     int mi = 0x7fffffff;
 #pragma unroll
     for (int j = 0; j < NJ4; ++j) {
       const int c = 4 * lane + 256 * j;
       if (c < P) {
-        const f32x4 x = ld4(logits + base + c);
         float E[4];
-        if (exp_noise) {
+        if constexpr (NOISE) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) E[e] = exp_noise[((int64_t)b * P + c + e) * HW + pix];   // NCHW draw
         } else {
@@ -307,14 +345,23 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          z[j][e] = (x[e] - logf(E[e])) * inv_tau;
-          if (z[j][e] > m) { m = z[j][e]; mi = c + e; }
+          const float zv = (xc[j][e] - logf(E[e])) * inv_tau;
+          if constexpr (SOFT) {
+            z[j][e] = zv;
+            if (zv > m) { m = zv; mi = c + e; }
+          } else {
+            const bool up = zv > m;
+            const float d = expf(up ? m - zv : zv - m);      // exp(-|zv - m|); exp(-inf) = 0 first
+            ls = up ? fmaf(ls, d, 1.0f) : ls + d;
+            if (up) { m = zv; mi = c + e; }
+          }
         }
-      } else {
+      } else if constexpr (SOFT) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) z[j][e] = -INFINITY;
       }
     }
+    const float lm = m;
     // wave argmax, first index on ties
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -323,14 +370,18 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
       if (om > m || (om == m && oi < mi)) { m = om; mi = oi; }
     }
     float sum = 0.f;
+    if constexpr (SOFT) {
 #pragma unroll
-    for (int j = 0; j < NJ4; ++j)
+      for (int j = 0; j < NJ4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float ez = (4 * lane + 256 * j < P) ? expf(z[j][e] - m) : 0.f;
-        if constexpr (SOFT) z[j][e] = ez;
-        sum += ez;
-      }
+        for (int e = 0; e < 4; ++e) {
+          const float ez = (4 * lane + 256 * j < P) ? expf(z[j][e] - m) : 0.f;
+          z[j][e] = ez;
+          sum += ez;
+        }
+    } else {
+      sum = lm == -INFINITY ? 0.f : ls * expf(lm - m);
+    }
     if constexpr (SOFT) {
       const float inv = 1.0f / wave_sum(sum);
 #pragma unroll
@@ -489,11 +540,11 @@ extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, 
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,
                                         int apply_thresh, float thresh, float* x_out, float* out, void* stream) {
-  if (B < 0 || D <= 0 || K <= 0 || D > 16384 || !x || !W || !out) return PIPNET_ERR_ARG;
+  if (B < 0 || D <= 0 || K <= 0 || !x || !W || !out) return PIPNET_ERR_ARG;
   if (B == 0) return PIPNET_OK;
   if ((D & 3) == 0 && (!aligned16(W) || !aligned16(x))) return PIPNET_ERR_ALIGN;
   const dim3 grid(B, (K + NN_CLS_PER_BLOCK - 1) / NN_CLS_PER_BLOCK);
-  hipLaunchKernelGGL(nonneg_linear_kernel, grid, dim3(HEAD_THREADS), sizeof(float) * D, (hipStream_t)stream, x,
+  hipLaunchKernelGGL(nonneg_linear_kernel, grid, dim3(HEAD_THREADS), 0, (hipStream_t)stream, x,
                      D, W, bias, K, apply_thresh, thresh, x_out, out);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
@@ -509,11 +560,15 @@ int count_gumbel_launch(const float* logits, int B, int HW, int P, float tau, co
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (!zero_fill(hist, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
-  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const dim3 grid((HW + CG_PIX_PER_BLOCK - 1) / CG_PIX_PER_BLOCK, B);
   const float inv_tau = 1.0f / tau;
 #define CG_CALL(N)                                                                                              \
-  hipLaunchKernelGGL((count_gumbel_kernel<N>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, exp_noise, \
-                     seed, offset, seed_dev, proto, hist);
+  if (exp_noise)                                                                                                \
+    hipLaunchKernelGGL((count_gumbel_kernel<N, false, true>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, \
+                       exp_noise, seed, offset, seed_dev, proto, hist);                                          \
+  else                                                                                                          \
+    hipLaunchKernelGGL((count_gumbel_kernel<N, false, false>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, \
+                       exp_noise, seed, offset, seed_dev, proto, hist);
   PIPNET_NJ_SWITCH(nj, CG_CALL)
 #undef CG_CALL
   PIPNET_CHECK_LAUNCH();
@@ -555,11 +610,15 @@ extern "C" int pipnet_count_gumbel_soft_f32(const float* logits, int B, int HW, 
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (!zero_fill(reinterpret_cast<uint32_t*>(sums), (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
-  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const dim3 grid((HW + CG_PIX_PER_BLOCK - 1) / CG_PIX_PER_BLOCK, B);
   const float inv_tau = 1.0f / tau;
 #define CG_CALL(N)                                                                                                \
-  hipLaunchKernelGGL((count_gumbel_kernel<N, true>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau,      \
-                     exp_noise, seed, offset, nullptr, proto, nullptr, sums);
+  if (exp_noise)                                                                                                  \
+    hipLaunchKernelGGL((count_gumbel_kernel<N, true, true>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, \
+                       exp_noise, seed, offset, nullptr, proto, nullptr, sums);                                    \
+  else                                                                                                            \
+    hipLaunchKernelGGL((count_gumbel_kernel<N, true, false>), grid, dim3(HEAD_THREADS), 0, s, logits, HW, P, inv_tau, \
+                       exp_noise, seed, offset, nullptr, proto, nullptr, sums);
   PIPNET_NJ_SWITCH(nj, CG_CALL)
 #undef CG_CALL
   PIPNET_CHECK_LAUNCH();

@@ -8,6 +8,8 @@ from __future__ import annotations
 
 from typing import Optional, Tuple
 
+import os
+
 import torch
 
 from . import _lib
@@ -45,15 +47,20 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
 
 
+SPLITK_WG_PER_CU = int(os.environ.get("PIPNET_SPLITK_WG_PER_CU", "2"))   # env: A/B runs (tools)
+
+
 def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
-    """K slabs for short-M GEMMs: enough workgroups to cover every CU at least once, each
-    slab >= 8 K-tiles of 32 (the Bilinear intermediate at M = batch has only 48 tiles)."""
+    """K slabs for short-M GEMMs, which stream their weights once (C5's Bilinear intermediate
+    at M = batch: 48 tiles of 64 x 128 over 151 MB of W / V): enough workgroups for
+    SPLITK_WG_PER_CU per CU -- about 100 KB of LDS-DMA in flight per CU, what HBM latency
+    needs -- each slab >= 8 K-tiles of 32."""
     if n % 4 or k % 32 or m > 512:     # backbone GEMMs (M = pixels) stay batch-invariant
         return 1
     tiles = -(-m // 64) * -(-n // 128)
     if tiles >= cus:
         return 1
-    return max(1, min(-(-cus // tiles), k // 256, 64))
+    return max(1, min(-(-SPLITK_WG_PER_CU * cus // tiles), k // 256, 64))
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:

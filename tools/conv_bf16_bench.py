@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None, help="comma-separated layer names")
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5")
+    ap.add_argument("--lib", action="store_true",
+                    help="also time the vendor library on the same shape (torch bf16: hipBLASLt GEMM for 1x1 "
+                         "convs, MIOpen channels_last conv otherwise) as a reference ceiling")
     a = ap.parse_args()
     build.build()
     dev = torch.device("cuda:0")
@@ -73,9 +76,37 @@ def main():
             ms = e0.elapsed_time(e1) / a.reps
             total[t] += ms * cnt
             line += f"  t{t}: {flops / ms / 1e9:6.1f} TF ({ms * 1e3:6.0f} us)"
+        if a.lib:
+            ms = _time_lib(x, w.shape, cout, k, s, pad, a.reps, dev)
+            total.setdefault("lib", 0.0)
+            total["lib"] += ms * cnt
+            line += f"  lib: {flops / ms / 1e9:6.1f} TF ({ms * 1e3:6.0f} us)"
         print(line, flush=True)
     print("network conv time (ms, sum over layers x count):",
           " ".join(f"t{t}={v:.2f}" for t, v in total.items()), flush=True)
+
+
+def _time_lib(x, wshape, cout, k, s, pad, reps, dev):
+    """Vendor-library time of the same conv (no fused epilogue): hipBLASLt for 1x1 stride-1,
+    MIOpen (torch conv2d, channels_last bf16) otherwise."""
+    b, h, _, cin = x.shape
+    if k == 1 and s == 1:
+        a2 = x.reshape(-1, cin)
+        wt = torch.randn(cout, cin, device=dev).to(torch.bfloat16)
+        fn = lambda: torch.nn.functional.linear(a2, wt)      # noqa: E731
+    else:
+        xc = x.permute(0, 3, 1, 2)                             # NCHW view of NHWC storage = channels_last
+        wt = torch.randn(cout, cin, k, k, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        fn = lambda: torch.nn.functional.conv2d(xc, wt, stride=s, padding=pad)    # noqa: E731
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
 
 
 if __name__ == "__main__":
