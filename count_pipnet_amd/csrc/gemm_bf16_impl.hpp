@@ -439,12 +439,14 @@ typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
 namespace pp {
-constexpr int BM = 256, BN = 256, BK = 32, NS = 4, NT = 512;
+constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
 constexpr int ROWB = BK * 2;                          // 64 B per LDS row
 constexpr int STAGE_BYTES = (BM + BN) * ROWB;         // 32 KiB
 constexpr int EPI_LD = 68;                            // fp32 epilogue rows: 64 + 4 pad
 constexpr int EPI_BYTES = 8 * 64 * EPI_LD * 4;        // 8 waves x 64 rows
-constexpr int SMEM_BYTES = NS * STAGE_BYTES > EPI_BYTES ? NS * STAGE_BYTES : EPI_BYTES;
+// DB = prefetch distance of B in K-tiles (A: DB + 1), NS = DB + 2 LDS stages of 32 KiB
+template <int DB>
+constexpr int smem_bytes() { return (DB + 2) * STAGE_BYTES > EPI_BYTES ? (DB + 2) * STAGE_BYTES : EPI_BYTES; }
 PIPNET_DEV int g(int r) { return (-(r >> 2)) & 3; }
 }  // namespace pp
 
@@ -452,146 +454,33 @@ template <int NPEND>
 PIPNET_DEV void pp_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPEND) : "memory");
 }
+// runtime (wave-uniform) count -> immediate: the counts are even and <= 4 DB - 2
+PIPNET_DEV void pp_wait_vm_dyn(int n) {
+  switch (n) {
+    case 0: pp_wait_vm<0>(); break;
+    case 2: pp_wait_vm<2>(); break;
+    case 4: pp_wait_vm<4>(); break;
+    case 6: pp_wait_vm<6>(); break;
+    case 8: pp_wait_vm<8>(); break;
+    case 10: pp_wait_vm<10>(); break;
+    default: pp_wait_vm<0>(); break;
+  }
+}
 PIPNET_DEV void pp_barrier() {
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// NB = B fragments (16 columns each) per wave: 4 -> 256-wide tiles, 3 -> 192-wide (N = 384 /
-// 192 layers: two 192-wide tiles instead of a full and a half-empty 256-wide one).  The DMA
-// and LDS layout stay those of the 256-wide tile (rows 192..255 are fetched and unused), so
-// the vmcnt accounting is identical.
-template <int EPI, int ALOAD, int NB = 4>
-__global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
+// Epilogue of the 256-row ping-pong tiles: per row half, the wave's fp32 accumulators are
+// re-laid through its own LDS rows (64 x 68 floats), then every lane finishes 8 consecutive
+// channels of one pixel (bias, residual, ReLU or the split-bf16 forms) with 16-B accesses.
+// The stage buffers must be free (all waves past the main loop's last barrier).
+template <int EPI, int NB>
+PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], unsigned char* smem, int m0, int n0,
+                            int wr, int wc, int lane, int wid) {
   using namespace pp;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wid = tid >> 6;
-  const int wr = wid >> 2, wc = wid & 3;
-  int m0, n0;
-  static_assert(NB == 3 || NB == 4, "NB");
-  constexpr int WCOLS = 16 * NB;                               // output columns per wave
-  tile_coords(p, BM, 4 * WCOLS, m0, n0);
-  const int nk = p.K / BK;
-
-  // ---- DMA sources: pieces wid and wid + 8 of A and of B (16 rows x 64 B each) ----
-  const int drow = lane >> 2;                                  // row within a piece
-  const int dchunk = 8 * ((lane & 3) ^ g(drow));               // logical chunk (elements)
-  ARow ar[2];
-  const bf16* wsrc[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * (wid + 8 * i) + drow;
-    ar[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
-    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
-  }
-  // (tap, channel) of the K-tile the DMA fetches next, advanced incrementally (a 32-deep
-  // K-tile never straddles a tap: Cin % 32 == 0), so no division in the loop.
-  int d_c = 0, d_kx = 0, d_ky = 0;
-  auto a_src = [&](const ARow& r, int k0) -> const void* {
-    if (k0 >= p.Kv) return g_zero_bf;
-    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k0) + dchunk;
-    const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
-    if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
-    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, d_c) + dchunk;
-  };
-  auto advance = [&]() {
-    if (ALOAD != ALOAD_DENSE) {
-      d_c += BK;
-      if (d_c == p.Cin) {
-        d_c = 0;
-        if (++d_kx == p.KW) d_kx = 0, ++d_ky;
-      }
-    }
-  };
-  auto stage_a = [&](int kt) {                                 // 2 x 1 KiB A pieces of this wave
-    unsigned char* base = smem + (kt & (NS - 1)) * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a_src(ar[i], kt * BK),
-                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
-                                       0, 0);
-    advance();
-  };
-  auto stage_b = [&](int kt) {                                 // 2 x 1 KiB B pieces of this wave
-    unsigned char* base = smem + (kt & (NS - 1)) * STAGE_BYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
-                                       (__attribute__((address_space(3))) void*)(base + BM * ROWB +
-                                                                                 (wid + 8 * i) * 1024),
-                                       16, 0, 0);
-  };
-  // ---- fragment reads: lane reads row (l & 15) of a 16-row block, logical chunk l >> 4 ----
+  constexpr int WCOLS = 16 * NB;
   const int fr = lane & 15;
-  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));     // byte offset inside a 16-row block
-  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
-  };
-  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
-#pragma unroll
-    for (int n = 0; n < NB; ++n)
-      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * WCOLS + n * 16) * ROWB + fofs);
-  };
-
-  f32x4v acc[8][NB];
-#pragma unroll
-  for (int r = 0; r < 8; ++r)
-#pragma unroll
-    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-  // prologue: A(0) B(0) A(1) B(1) A(2) in flight (B(kt+2) is fetched in phase 0 of K-tile
-  // kt, A(kt+3) in phase 1: two pieces per phase), wait for tile 0
-  stage_a(0), stage_b(0);
-  if (nk > 1) stage_a(1), stage_b(1);
-  if (nk > 2) stage_a(2);
-  if (nk > 2) pp_wait_vm<6>();
-  else if (nk == 2) pp_wait_vm<4>();
-  else pp_wait_vm<0>();
-  pp_barrier();
-  if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
-
-  bf16x8v fa[4], fb[4];
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* st = smem + (kt & (NS - 1)) * STAGE_BYTES;
-    // ---- phase 0: rows 0..63 of the wave's block ----
-    if (kt + 2 < nk) stage_b(kt + 2);                          // DMA before the reads (M0 write)
-    read_b(fb, st);
-    read_a(fa, st, 0);
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int n = 0; n < NB; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    // ---- phase 1: rows 64..127; fetch A of K-tile kt+3 (DMA first: an M0 write for the DMA
-    // would otherwise wait for this phase's fragment reads); wait for K-tile kt+1 ----
-    if (kt + 3 < nk) stage_a(kt + 3);
-    read_a(fa, st, 1);
-    // pieces issued after B(kt+1) (the last of K-tile kt+1): A(kt+2), B(kt+2), A(kt+3)
-    if (kt + 3 < nk) pp_wait_vm<6>();
-    else if (kt + 2 < nk) pp_wait_vm<4>();
-    else pp_wait_vm<0>();
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int n = 0; n < NB; ++n)
-        acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-  }
-  if (wr == 0) pp_barrier();                                   // re-align the groups
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  pp_barrier();                                                // stage buffers free for the epilogue
-
-  // ---- epilogue: per row half, fp32 re-layout in the wave's own LDS rows, then 8 channels per lane ----
   constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
   float* wt = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
   const int c8 = lane & 7;
@@ -660,6 +549,175 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // reads done before the next half's writes
   }
+}
+
+// NB = B fragments (16 columns each) per wave: 4 -> 256-wide tiles, 3 -> 192-wide (N = 384 /
+// 192 layers: two 192-wide tiles instead of a full and a half-empty 256-wide one).  The DMA
+// and LDS layout stay those of the 256-wide tile (rows 192..255 are fetched and unused), so
+// the vmcnt accounting is identical.
+// ABL (tuning lab only, tools/bf16_lab.hip; 0 in the product): 1 = no LDS-DMA (stale LDS, no
+// vmcnt waits), 2 = no epilogue (one store per lane keeps the accumulators live), 4 = no
+// barriers, 8 = no fragment reads after the first (stale registers).
+template <int EPI, int ALOAD, int NB = 4, int ABL = 0, int DB = 2>
+__global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
+  using namespace pp;
+  constexpr int NS = DB + 2;
+  static_assert(DB >= 2 && DB <= 3, "DB");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[smem_bytes<DB>()];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  static_assert(NB == 3 || NB == 4, "NB");
+  constexpr int WCOLS = 16 * NB;                               // output columns per wave
+  tile_coords(p, BM, 4 * WCOLS, m0, n0);
+  const int nk = p.K / BK;
+
+  // ---- DMA sources: pieces wid and wid + 8 of A and of B (16 rows x 64 B each) ----
+  const int drow = lane >> 2;                                  // row within a piece
+  const int dchunk = 8 * ((lane & 3) ^ g(drow));               // logical chunk (elements)
+  ARow ar[2];
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (wid + 8 * i) + drow;
+    ar[i] = a_row<ALOAD>(p, min(m0 + row, p.M - 1));
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
+  }
+  // (tap, channel) of the K-tile the DMA fetches next, advanced incrementally (a 32-deep
+  // K-tile never straddles a tap: Cin % 32 == 0), so no division in the loop.
+  int d_c = 0, d_kx = 0, d_ky = 0;
+  auto a_src = [&](const ARow& r, int k0) -> const void* {
+    if (k0 >= p.Kv) return g_zero_bf;
+    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k0) + dchunk;
+    const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
+    if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
+    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, d_c) + dchunk;
+  };
+  auto advance = [&]() {
+    if (ALOAD != ALOAD_DENSE) {
+      d_c += BK;
+      if (d_c == p.Cin) {
+        d_c = 0;
+        if (++d_kx == p.KW) d_kx = 0, ++d_ky;
+      }
+    }
+  };
+  auto stage_a = [&](int kt) {                                 // 2 x 1 KiB A pieces of this wave
+    if constexpr ((ABL & 1) != 0) return;
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)a_src(ar[i], kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
+                                       0, 0);
+    advance();
+  };
+  auto stage_b = [&](int kt) {                                 // 2 x 1 KiB B pieces of this wave
+    if constexpr ((ABL & 1) != 0) return;
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + BM * ROWB +
+                                                                                 (wid + 8 * i) * 1024),
+                                       16, 0, 0);
+  };
+  // ---- fragment reads: lane reads row (l & 15) of a 16-row block, logical chunk l >> 4 ----
+  const int fr = lane & 15;
+  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));     // byte offset inside a 16-row block
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
+    if constexpr ((ABL & 8) != 0) {
+      if (st != smem || half != 0) return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
+  };
+  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
+    if constexpr ((ABL & 8) != 0) {
+      if (st != smem) return;
+    }
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * WCOLS + n * 16) * ROWB + fofs);
+  };
+
+  f32x4v acc[8][NB];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  // pieces (2 per operand tile per wave) issued after B(kt + 1) by the end of phase 1 of K-tile kt:
+  // A(j), B(j) for j = kt+2 .. kt+DB and A(kt+DB+1), those that exist
+  auto younger_than_b = [&](int kt) {
+    int n = 0;
+#pragma unroll
+    for (int j = 2; j <= DB; ++j) n += (kt + j < nk) ? 4 : 0;
+    return n + ((kt + DB + 1 < nk) ? 2 : 0);
+  };
+  // prologue: A(0) B(0) .. A(DB-1) B(DB-1) A(DB) in flight (B(kt+DB) is fetched in phase 0 of
+  // K-tile kt, A(kt+DB+1) in phase 1: two pieces per phase), wait for tile 0
+#pragma unroll
+  for (int i = 0; i < DB; ++i)
+    if (i < nk) stage_a(i), stage_b(i);
+  if (DB < nk) stage_a(DB);
+  pp_wait_vm_dyn(younger_than_b(-1));
+  pp_barrier();
+  if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
+
+  auto bar = [&]() {
+    if constexpr ((ABL & 4) == 0) pp_barrier();
+  };
+  bf16x8v fa[4], fb[4];
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+    // ---- phase 0: rows 0..63 of the wave's block ----
+    if (kt + DB < nk) stage_b(kt + DB);                        // DMA before the reads (M0 write)
+    read_b(fb, st);
+    read_a(fa, st, 0);
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+    // ---- phase 1: rows 64..127; fetch A of K-tile kt+3 (DMA first: an M0 write for the DMA
+    // would otherwise wait for this phase's fragment reads); wait for K-tile kt+1 ----
+    if (kt + DB + 1 < nk) stage_a(kt + DB + 1);
+    read_a(fa, st, 1);
+    // wait for this wave's pieces of K-tile kt+1 (B(kt+1) is its last)
+    if constexpr ((ABL & 1) == 0) pp_wait_vm_dyn(younger_than_b(kt));
+    bar();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    bar();
+  }
+  if (wr == 0) pp_barrier();                                   // re-align the groups
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pp_barrier();                                                // stage buffers free for the epilogue
+  if constexpr ((ABL & 2) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += acc[r][n][i];
+    reinterpret_cast<float*>(p.C)[(int64_t)blockIdx.x * pp::NT + tid] = t;
+    return;
+  }
+
+  pp_epilogue<EPI, NB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
 }
 
 }  // namespace pipnet_bf16

@@ -1,0 +1,267 @@
+// Tuning lab for the bf16 GEMM tiles (not part of the product library): the product's
+// ping-pong kernel (gemm_bf16_impl.hpp) instantiated with its ABL ablation switches on a
+// dense GEMM C[M][N] = A[M][K] W[N][K]^T (bf16 in / out, fp32 accumulation).
+// Built by tools/bf16_lab.py into tools/libbf16_lab.so.
+#include "../count_pipnet_amd/csrc/gemm_bf16_impl.hpp"
+
+using namespace pipnet_bf16;
+
+namespace pipnet_bf16 {
+// Lab-only kernel (measured, not adopted: profiles/r02/bf16_lab.txt): ABL bits as the product
+// kernel's, plus 16 = every DMA re-reads K-tile 0 (cache-hot sources), 32 = no A DMA (B only).
+// ======================================================================================
+// 256x256 ping-pong tile with 64-deep K-tiles in full 128-B LDS rows (tile 8).
+//
+// Same wave roles as conv_bf16_pp_kernel (8 waves = 2 row groups x 4 column blocks, wave
+// (wr, wc) owns rows wr*128.., cols wc*64.. as 8 x 4 MFMA 16x16 tiles, group 1 one barrier
+// behind group 0) but every LDS-DMA piece moves 8 whole 128-B lines (8 rows x 64 k) instead
+// of 16 half lines: half the TA / L2 requests per byte (cdna_hip_programming.md 5, x through
+// LDS in full lines).  A K-tile is four PHASES of 16 MFMAs, ordered so that the operands
+// free up early:
+//     q0 = (rows r0, k 0..31)   reads B[k0] (4) + A[r0,k0] (4)
+//     q1 = (rows r0, k 32..63)  reads B[k1] (4) + A[r0,k1] (4)
+//     q2 = (rows r1, k 0..31)   reads A[r1,k0] (4), B[k0] kept in registers
+//     q3 = (rows r1, k 32..63)  reads A[r1,k1] (4), B[k1] kept in registers
+// (r0 / r1 = the first / last 64 rows of a wave's 128).  So B and the r0 A rows of K-tile t
+// are dead after phase q1 of t, the r1 A rows after q3.  Two LDS stages of 64 KiB (tile t in
+// stage t & 1) then give each piece a long flight: per wave and phase one 2-piece item,
+//     (t,0): A_r0(t+1)   (t,1): A_r1(t+1)   (t,2): B(t+2) first half   (t,3): B(t+2) second half
+// -- B(t+2) lands in stage t & 1 once B(t) is dead, A(t+1) in the other stage once K-tile t-1
+// is dead.  Waits (counted vmcnt, in the load segment, after that phase's DMA issue):
+//     (t-1,3): B(t), A_r0(t)    younger: A_r1(t), B(t+1) x2          -> 6 (2 if t+1 = nk)
+//     (t,1)  : A_r1(t)          younger: B(t+1) x2, A_r0/A_r1(t+1)   -> 8 (0 if t+1 = nk)
+// Every load segment ends with lgkmcnt(0) before its barrier, so a region's last reads have
+// completed at the barrier after which the next DMA into it is issued (WAR), and every
+// wave's wait precedes a barrier that the readers pass (RAW; group 1 one barrier later).
+// Swizzle: logical 16-B chunk c of row r at physical chunk c ^ (r & 7): conflict-free for
+// the 16x16x32 fragment reads (lane l: row l & 15, chunk 4 s + (l >> 4)); the DMA writes
+// lane-linear, so the inverse is applied to its source address.
+// Requirements: K % 64 == 0 (packed weights), Cin % 64 == 0 for the implicit conv (a K-tile
+// never straddles two taps), N % 8 == 0.
+// ======================================================================================
+namespace p64 {
+constexpr int BM = 256, BN = 256, BK = 64, NT = 512;
+constexpr int ROWB = 128;                                     // one LDS row = 64 bf16
+constexpr int A_BYTES = BM * ROWB, STAGE_BYTES = (BM + BN) * ROWB;   // 32 + 32 KiB
+constexpr int SMEM_BYTES = 2 * STAGE_BYTES > pp::EPI_BYTES ? 2 * STAGE_BYTES : pp::EPI_BYTES;
+}  // namespace p64
+
+template <int EPI, int ALOAD, int ABL = 0, int CPA = 0, int CPB = 0>   // CPA / CPB: cache-policy bits of the A / B LDS-DMA
+__global__ __launch_bounds__(p64::NT, 1) void conv_bf16_p64_kernel(ConvParams p) {
+  using namespace p64;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  tile_coords(p, BM, BN, m0, n0);
+  const int nk = p.K / BK;
+
+  // ---- DMA: lane L of a piece writes row (L >> 3) of its 8, physical chunk L & 7 ----
+  const int drow = lane >> 3;
+  const int dchunk = 8 * ((lane & 7) ^ drow);                  // logical chunk (elements); row & 7 = drow
+  // A pieces of this wave: r0 rows = pieces wid, 16 + wid; r1 rows = pieces 8 + wid, 24 + wid
+  ARow ar[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int piece = (i & 1) * 8 + (i >> 1) * 16 + wid;     // i: 0 = r0a, 1 = r1a, 2 = r0b, 3 = r1b
+    ar[i] = a_row<ALOAD>(p, min(m0 + 8 * piece + drow, p.M - 1));
+  }
+  // B pieces of this wave: wid, 8 + wid (first half), 16 + wid, 24 + wid (second half)
+  const bf16* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wsrc[i] = p.W + (int64_t)min(n0 + 8 * (8 * i + wid) + drow, p.N - 1) * p.K + dchunk;
+  // (tap, channel) of the A K-tile being staged (both of its items), advanced after its r1 item
+  int d_c = 0, d_kx = 0, d_ky = 0;
+  auto a_src = [&](const ARow& r, int k0) -> const void* {
+    if (k0 >= p.Kv) return g_zero_bf;
+    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k0) + dchunk;
+    const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
+    if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
+    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, d_c) + dchunk;
+  };
+  auto dma = [&](const void* src, unsigned char* dst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, CPA);
+  };
+  auto dmab = [&](const void* src, unsigned char* dst) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, CPB);
+  };
+  auto stage_a = [&](int kt, int half) {                      // half 0 = r0 rows, 1 = r1 rows
+    if constexpr ((ABL & 1) != 0) return;
+    unsigned char* base = smem + (kt & 1) * STAGE_BYTES;
+    if constexpr ((ABL & 16) != 0) kt = 0;                    // lab: always the first K-tile (cache-hot)
+    if constexpr ((ABL & 32) != 0) return;                    // lab: B operand only
+    dma(a_src(ar[half], kt * BK), base + (half * 8 + wid) * 1024);
+    dma(a_src(ar[2 + half], kt * BK), base + (half * 8 + 16 + wid) * 1024);
+    if (half == 1 && ALOAD != ALOAD_DENSE) {
+      d_c += BK;
+      if (d_c == p.Cin) {
+        d_c = 0;
+        if (++d_kx == p.KW) d_kx = 0, ++d_ky;
+      }
+    }
+  };
+  auto stage_b = [&](int kt, int half) {                      // half 0 = pieces wid, 8 + wid
+    if constexpr ((ABL & 1) != 0) return;
+    unsigned char* base = smem + (kt & 1) * STAGE_BYTES + A_BYTES;
+    if constexpr ((ABL & 16) != 0) kt = 0;
+    dmab(wsrc[2 * half] + kt * BK, base + (16 * half + wid) * 1024);
+    dmab(wsrc[2 * half + 1] + kt * BK, base + (16 * half + 8 + wid) * 1024);
+  };
+  // ---- fragments: lane reads row (l & 15) of a 16-row block, logical chunk 4 s + (l >> 4) ----
+  const int fr = lane & 15;
+  const int fofs0 = fr * ROWB + 16 * ((lane >> 4) ^ (fr & 7));          // k-step s = 0
+  const int fofs1 = fr * ROWB + 16 * ((4 + (lane >> 4)) ^ (fr & 7));    // k-step s = 1
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int rh, int s) {
+    if constexpr ((ABL & 8) != 0) {
+      if (st != smem || rh != 0) return;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + rh * 64 + r * 16) * ROWB + (s ? fofs1 : fofs0));
+  };
+  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st, int s) {
+    if constexpr ((ABL & 8) != 0) {
+      if (st != smem) return;
+    }
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + (wc * 64 + n * 16) * ROWB + (s ? fofs1 : fofs0));
+  };
+  auto bar = [&]() {
+    if constexpr ((ABL & 4) == 0) pp_barrier();
+  };
+  auto wait_vm = [&](int n) {
+    if constexpr ((ABL & 32) != 0) {
+      pp_wait_vm_dyn(n >= 8 ? 4 : (n >= 6 ? 4 : 0));          // lab: B-only counts (conservative)
+    } else if constexpr ((ABL & 1) == 0) {
+      pp_wait_vm_dyn(n);
+    }
+  };
+  auto reads_done = [&]() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+
+  f32x4v acc[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  auto mfma16 = [&](const bf16x8v (&fa)[4], const bf16x8v (&fb)[4], int rh) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[rh * 4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[rh * 4 + r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: B(0), A_r0(0), A_r1(0), B(1) in flight; wait for B(0), A_r0(0)
+  stage_b(0, 0), stage_b(0, 1), stage_a(0, 0), stage_a(0, 1);
+  if (nk > 1) stage_b(1, 0), stage_b(1, 1);
+  wait_vm(nk > 1 ? 6 : 2);
+  reads_done();
+  pp_barrier();
+  if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
+
+  bf16x8v fa[4], fb0[4], fb1[4];
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* st = smem + (kt & 1) * STAGE_BYTES;
+    const bool more = kt + 1 < nk;
+    // ---- q0: rows r0, k 0..31; stage A_r0(kt+1) ----
+    if (more) stage_a(kt + 1, 0);
+    read_b(fb0, st, 0);
+    read_a(fa, st, 0, 0);
+    reads_done();
+    bar();
+    mfma16(fa, fb0, 0);
+    bar();
+    // ---- q1: rows r0, k 32..63; stage A_r1(kt+1); wait for A_r1(kt) ----
+    if (more) stage_a(kt + 1, 1);
+    read_b(fb1, st, 1);
+    read_a(fa, st, 0, 1);
+    wait_vm(more ? 8 : 0);
+    reads_done();
+    bar();
+    mfma16(fa, fb1, 0);
+    bar();
+    // ---- q2: rows r1, k 0..31; stage B(kt+2) first half (B(kt) is dead) ----
+    if (kt + 2 < nk) stage_b(kt + 2, 0);
+    read_a(fa, st, 1, 0);
+    reads_done();
+    bar();
+    mfma16(fa, fb0, 1);
+    bar();
+    // ---- q3: rows r1, k 32..63; stage B(kt+2) second half; wait for B(kt+1), A_r0(kt+1) ----
+    if (kt + 2 < nk) stage_b(kt + 2, 1);
+    read_a(fa, st, 1, 1);
+    if (more) wait_vm(kt + 2 < nk ? 6 : 2);
+    reads_done();
+    bar();
+    mfma16(fa, fb1, 1);
+    bar();
+  }
+  if (wr == 0) pp_barrier();                                   // re-align the groups
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  pp_barrier();                                                // stage buffers free for the epilogue
+  if constexpr ((ABL & 2) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += acc[r][n][i];
+    reinterpret_cast<float*>(p.C)[(int64_t)blockIdx.x * p64::NT + tid] = t;
+    return;
+  }
+  pp_epilogue<EPI, 4>(p, acc, smem, m0, n0, wr, wc, lane, wid);
+}
+
+}  // namespace pipnet_bf16
+
+namespace {
+int group_for(int K, double budget) {
+  const double panel = 128.0 * K * 2.0;
+  int g = (int)(budget / panel);
+  return g < 1 ? 1 : (g > 16 ? 16 : g);
+}
+}  // namespace
+
+extern "C" int lab_pp(int abl, const void* A, const void* W, void* C, int M, int N, int K, double group_budget,
+                      void* stream) {
+  ConvParams p{};
+  p.A = reinterpret_cast<const bf16*>(A);
+  p.lda = K;
+  p.W = reinterpret_cast<const bf16*>(W);
+  p.C = reinterpret_cast<bf16*>(C);
+  p.ldc = N;
+  p.M = M; p.N = N; p.K = K; p.Kv = K;
+  p.Cin = K; p.Cinp = K; p.H = 1; p.Wd = 1; p.OH = 1; p.OW = 1; p.stride = 1; p.KW = 1;
+  p.nt = (N + 255) / 256;
+  p.mt = (M + 255) / 256;
+  p.group_m = group_for(K, group_budget);
+  const dim3 grid(p.mt * p.nt);
+  hipStream_t s = (hipStream_t)stream;
+  // abl = ablation bits (0..15) + 16 * (DB - 2) for the 32-deep ping-pong kernel; 32 + bits
+  // for the 64-deep full-line kernel (conv_bf16_p64_kernel)
+#define LAB_CASE(X, D) \
+  case X + 16 * (D - 2): hipLaunchKernelGGL((conv_bf16_pp_kernel<PIPNET_EPI_NONE, ALOAD_DENSE, 4, X, D>), grid, dim3(512), 0, s, p); break;
+#define LAB_P64(X) \
+  case 32 + X: hipLaunchKernelGGL((conv_bf16_p64_kernel<PIPNET_EPI_NONE, ALOAD_DENSE, X>), grid, dim3(512), 0, s, p); break;
+  // 128 + cpolicy index: p64 with LDS-DMA cache-policy bits (A, B)
+#define LAB_CP(I, A_, B_) \
+  case 128 + I: hipLaunchKernelGGL((conv_bf16_p64_kernel<PIPNET_EPI_NONE, ALOAD_DENSE, 0, A_, B_>), grid, dim3(512), 0, s, p); break;
+  switch (abl) {
+    LAB_CP(0, 0, 0) LAB_CP(1, 1, 1) LAB_CP(2, 2, 2) LAB_CP(3, 16, 16) LAB_CP(4, 17, 17) LAB_CP(5, 2, 0)
+    LAB_CP(6, 0, 2) LAB_CP(7, 3, 3) LAB_CP(8, 16, 0) LAB_CP(9, 0, 16)
+    LAB_P64(0) LAB_P64(1) LAB_P64(2) LAB_P64(4) LAB_P64(8) LAB_P64(16) LAB_P64(18) LAB_P64(32) LAB_P64(34)
+    LAB_CASE(0, 2) LAB_CASE(1, 2) LAB_CASE(2, 2) LAB_CASE(4, 2) LAB_CASE(8, 2)
+    LAB_CASE(0, 3) LAB_CASE(1, 3) LAB_CASE(2, 3) LAB_CASE(4, 3) LAB_CASE(8, 3)
+    default: return 1;
+  }
+#undef LAB_CASE
+  return hipGetLastError() == hipSuccess ? 0 : 3;
+}
