@@ -81,6 +81,7 @@ SIGNATURES = {
     "pipnet_dwconv7_plain_f32": [P, I32, I32, I32, I32, P, P, I32, P, P],
     "pipnet_dwconv7_wgrad_f32": [P, P, I32, I32, I32, I32, P, P, I32, P, P],
     "pipnet_head_bwd_f32": [P, P, I32, I32, I32, P, P, I32, F32, F32, F32, P, P, P, P],
+    "pipnet_cnblock_mlp_f32": [P, P, P, P, P, P, P, I64, I32, P],
 }
 _RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64}
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, "pipnet_amd_source_digest": ctypes.c_char_p,

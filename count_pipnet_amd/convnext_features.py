@@ -234,6 +234,9 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
     return ent[1]
 
 
+FUSED_MLP = True      # tools / A-B runs may switch the fused narrow-stage MLP off
+
+
 def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Optional[Tensor] = None) -> Tensor:
     """One CNBlock in place on NHWC ``h``.  ``row_scale`` (train mode, StochasticDepth "row"):
     device [B] = keep_b / (1 - p); the Linear2 epilogue scales each sample's branch by it
@@ -246,8 +249,12 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
         raise RuntimeError(f"CNBlock {key}: unsupported depthwise conv {dw}")
     wdw = packed(cache, key + ".dw", dw.weight, lambda w: w.reshape(c, 49).t())
     t = K.dwconv7_ln(h, wdw, dw.bias, ln.weight, ln.bias)
-    u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS_GELU)
     hv = h.view(-1, c)
+    if row_scale is None and c in K.MLP_FUSED_CHANNELS and FUSED_MLP:
+        # narrow stages: Linear1 + GELU + Linear2 + layer_scale + residual in one kernel
+        K.cnblock_mlp(t.view(-1, c), l1.weight, l1.bias, l2.weight, l2.bias, blk.layer_scale.view(-1), hv)
+        return h
+    u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS_GELU)
     if row_scale is None:
         K.linear(u, l2.weight, l2.bias, _lib.EPI_RESID, scale=blk.layer_scale.view(-1), r=hv, out=hv)
     else:

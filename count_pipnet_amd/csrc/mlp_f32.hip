@@ -1,0 +1,191 @@
+// Fused CNBlock MLP of the narrow ConvNeXt stages (C = 96 / 192), exact fp32 on
+// v_mfma_f32_16x16x4_f32:
+//     x <- x + gamma * (W2 gelu(W1 t + b1) + b2)              (torchvision CNBlock, SURVEY.md 2.3:
+//                                                             block.3 Linear, block.4 GELU, block.5
+//                                                             Linear, layer_scale, + residual)
+// for NHWC rows t = dwconv+LN output [M, C], x = the residual stream [M, C] (updated in place).
+//
+// Why: at C = 96 / 192 the two Linears are K = 96 / N = 96-shaped GEMMs (49-57 % MFMA busy in
+// the unfused kernels) and the 4C-wide hidden activation makes an HBM round trip (308 MB per
+// stage-1 block at C2).  Here the hidden activation never leaves the registers:
+//
+//   * both products are computed TRANSPOSED, one wave per 16 pixels: GEMM1 h^T[hid][pix] =
+//     W1[hid][:] . t[pix][:] (A = W1 from LDS, B = t from registers), so the 16x16 result of
+//     one hidden block has the pixel on the lane and 4 hidden indices in the registers --
+//     exactly the B operand layout of GEMM2 out^T[c][pix] = W2[c][hid] . h^T[hid][pix] for 4
+//     k-steps (lane l supplies hidden 4(l>>4) + s at step s; the A operand W2[c][.] is read
+//     with the same index map: one float4 per lane per 4 MFMAs);
+//   * t stays in registers for the whole block (C/4 floats per lane), the accumulator of
+//     out^T (C/16 tiles x 4 floats) too; GELU (+ b1) is applied in registers;
+//   * the weights stream through LDS in hidden chunks of HC (W1 rows / W2 columns), double
+//     buffered by LDS-DMA (global_load_lds_dwordx4), XOR-swizzled 16-B chunks so that every
+//     ds_read_b128 lane group of the fragment reads hits 16 distinct bank slots;
+//   * epilogue: lane l owns pixel l & 15 and 4 consecutive channels per tile -> one float4
+//     read-modify-write of x per tile, with gamma and b2.
+// k order of both contractions: t / hidden index 16 g + 4 q + s (q = lane >> 4, MFMA step s)
+// -- a different (equally exact) fp32 summation order than the unfused GEMMs.
+#include "common.hpp"
+
+namespace {
+
+template <int C, int HC, int NW>
+struct MlpGeo {
+  static constexpr int NT = 64 * NW;
+  static constexpr int W1F = HC * C, W2F = C * HC, CHUNK_F = W1F + W2F;   // floats per chunk
+  static constexpr int NCH = 4 * C / HC;                                   // hidden chunks
+  static constexpr int W1_PIECES = W1F / 256, PIECES = CHUNK_F / 256;      // 1-KiB LDS-DMA pieces
+  static constexpr int PPW = PIECES / NW;                                  // pieces per wave
+  static constexpr int RC1 = C / 4, RC2 = HC / 4;                          // 16-B chunks per row
+  static_assert(C % 32 == 0 && RC1 % 8 == 0, "C");
+  static_assert(HC == 16 || HC == 32, "HC");
+  static_assert(PIECES % NW == 0 && W1F % 256 == 0 && W2F % 256 == 0, "pieces");
+  // chunk swizzles (XOR inside aligned groups of 16 / 8 / 4 chunks): conflict-free for the
+  // fragment reads (row = 16 blk + (l & 15), chunk = 4 g + (l >> 4)), checked exhaustively
+  static PIPNET_DEV int f1(int r) { return RC1 % 16 == 0 ? (r & 15) : (r & 7); }
+  static PIPNET_DEV int f2(int r) { return HC == 32 ? (r & 7) : ((r >> 1) & 3); }
+};
+
+template <int C, int HC, int NW>
+__global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
+                                                              const float* __restrict__ b1,
+                                                              const float* __restrict__ W2,
+                                                              const float* __restrict__ b2,
+                                                              const float* __restrict__ gamma, float* x, int M) {
+  using G = MlpGeo<C, HC, NW>;
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA early): two chunk
+  // buffers, then b1 (staged once: a per-chunk global load of it would wait for the DMA)
+  __shared__ __attribute__((aligned(16))) float smem[2 * G::CHUNK_F + 4 * C];
+  float* sb1 = smem + 2 * G::CHUNK_F;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int q = lane >> 4, pl = lane & 15;
+  const int pix = blockIdx.x * (16 * NW) + 16 * wid + pl;
+  const int prow = pix < M ? pix : M - 1;               // rows past M compute garbage, never stored
+
+  // ---- LDS-DMA sources of this wave's pieces (chunk 0); chunk c adds c*HC*C (W1) / c*HC (W2) ----
+  const float* src[G::PPW];
+  int dst[G::PPW];
+  bool is_w1[G::PPW];
+#pragma unroll
+  for (int j = 0; j < G::PPW; ++j) {
+    const int p = wid + NW * j;
+    dst[j] = p * 256;
+    if (p < G::W1_PIECES) {
+      const int e = p * 64 + lane;                        // 16-B chunk index inside the W1 image
+      const int r = e / G::RC1, pc = e - r * G::RC1;
+      src[j] = W1 + (int64_t)r * C + 4 * (pc ^ G::f1(r));
+      is_w1[j] = true;
+    } else {
+      const int e = (p - G::W1_PIECES) * 64 + lane;
+      const int r = e / G::RC2, pc = e - r * G::RC2;
+      src[j] = W2 + (int64_t)r * (4 * C) + 4 * (pc ^ G::f2(r));
+      is_w1[j] = false;
+    }
+  }
+  auto stage = [&](int ch) {
+    float* base = smem + (ch & 1) * G::CHUNK_F;
+#pragma unroll
+    for (int j = 0; j < G::PPW; ++j) {
+      const float* s = src[j] + (is_w1[j] ? (int64_t)ch * HC * C : (int64_t)ch * HC);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)s,
+                                       (__attribute__((address_space(3))) void*)(base + dst[j]), 16, 0, 0);
+    }
+  };
+  for (int i = tid; i < C; i += G::NT) st4(sb1 + 4 * i, ld4(b1 + 4 * i));
+  stage(0);
+
+  // ---- t of this lane's pixel in registers: tb[g] = t[pix][16 g + 4 q .. + 3] ----
+  f32x4 tb[C / 16];
+#pragma unroll
+  for (int g = 0; g < C / 16; ++g) tb[g] = ld4(t + (int64_t)prow * C + 16 * g + 4 * q);
+  f32x4 acc[C / 16];
+#pragma unroll
+  for (int cb = 0; cb < C / 16; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment offsets (floats) inside a chunk image
+  auto w1_off = [&](int hb, int g) {
+    const int r = 16 * hb + pl;
+    return r * C + 4 * ((4 * g + q) ^ G::f1(r));
+  };
+  auto w2_off = [&](int cb, int hb) {
+    const int r = 16 * cb + pl;
+    return G::W1F + r * HC + 4 * ((4 * hb + q) ^ G::f2(r));
+  };
+
+  for (int ch = 0; ch < G::NCH; ++ch) {
+    // this wave's pieces of chunk ch landed, every wave's reads of chunk ch-1 retired
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (ch + 1 < G::NCH) stage(ch + 1);                 // into the buffer of chunk ch-1
+    const float* buf = smem + (ch & 1) * G::CHUNK_F;
+    constexpr int NHB = HC / 16;
+    // GEMM1: h^T[16 hb + 4q + i][pixel] for the NHB hidden blocks of the chunk
+    f32x4 h[NHB];
+#pragma unroll
+    for (int hb = 0; hb < NHB; ++hb) h[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < C / 16; ++g) {
+#pragma unroll
+      for (int hb = 0; hb < NHB; ++hb) {
+        const f32x4 w = ld4(buf + w1_off(hb, g));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) h[hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s], tb[g][s], h[hb], 0, 0, 0);
+      }
+    }
+    // + b1, GELU (the unfused Linear1 epilogue's packed form)
+#pragma unroll
+    for (int hb = 0; hb < NHB; ++hb) {
+      const f32x4 bb = ld4(sb1 + ch * HC + 16 * hb + 4 * q);
+      const f32x4 v = h[hb] + bb;
+      const f32x2 lo = gelu_pk16(f32x2{v[0], v[1]}), hi = gelu_pk16(f32x2{v[2], v[3]});
+      h[hb] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+    }
+    // GEMM2: out^T[c][pixel] += W2[c][hidden] h^T[hidden][pixel]
+#pragma unroll
+    for (int cb = 0; cb < C / 16; ++cb) {
+#pragma unroll
+      for (int hb = 0; hb < NHB; ++hb) {
+        const f32x4 w = ld4(buf + w2_off(cb, hb));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s], h[hb][s], acc[cb], 0, 0, 0);
+      }
+    }
+  }
+  // ---- epilogue: x[pixel][c .. c+3] += gamma * (acc + b2), c = 16 cb + 4 q ----
+  if (pix < M) {
+    float* xr = x + (int64_t)pix * C;
+#pragma unroll
+    for (int cb = 0; cb < C / 16; ++cb) {
+      const int c = 16 * cb + 4 * q;
+      const f32x4 r = ld4(xr + c);
+      const f32x4 bb = ld4(b2 + c), gm = ld4(gamma + c);
+      st4(xr + c, r + gm * (acc[cb] + bb));
+    }
+  }
+}
+
+template <int C, int HC, int NW>
+int launch_mlp(const float* t, const float* W1, const float* b1, const float* W2, const float* b2, const float* gamma,
+               float* x, int M, hipStream_t s) {
+  const int px = 16 * NW;
+  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1, b1, W2,
+                     b2, gamma, x, M);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+}  // namespace
+
+extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2,
+                                      const float* b2, const float* gamma, float* x, int64_t M, int C,
+                                      void* stream) {
+  if (M < 0 || M >= ((int64_t)1 << 31) || (C != 96 && C != 192)) return PIPNET_ERR_ARG;
+  if (!t || !W1 || !b1 || !W2 || !b2 || !gamma || !x) return PIPNET_ERR_ARG;
+  if (!aligned16(t) || !aligned16(W1) || !aligned16(b1) || !aligned16(W2) || !aligned16(b2) || !aligned16(gamma) ||
+      !aligned16(x))
+    return PIPNET_ERR_ALIGN;
+  if (M == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (C == 96) return launch_mlp<96, 32, 8>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
+  return launch_mlp<192, 16, 4>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
+}

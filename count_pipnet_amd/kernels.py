@@ -228,9 +228,9 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     """rocprof name of the bf16 conv instantiation."""
     t = bf16_conv_tile(m, n, pp_ok, s3, kv) if tile < 0 else tile
     if t == 5:
-        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4>"
+        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4, 0, 2>"
     if t == 7:
-        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 3>"
+        return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 3, 0, 2>"
     cfg, minb = _BF16_CFG[t]
     npad = "true" if s3 and t == 4 and n % 128 else "false"     # padded-column MFMA blocks skipped
     return f"pipnet_bf16::conv_bf16_kernel<{cfg}, {epilogue}, {aload}, {minb}, {npad}>"
@@ -324,6 +324,30 @@ def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tens
     _lib.call("pipnet_convnext_stem_f32", x_nchw.data_ptr(), n, h, wd, w.data_ptr(), b.data_ptr(), ln_w.data_ptr(),
               ln_b.data_ptr(), y.data_ptr(), _stream(x_nchw))
     return y
+
+
+MLP_FUSED_CHANNELS = (96, 192)
+
+
+def cnblock_mlp_kernel_name(c: int) -> str:
+    return {96: "cnblock_mlp_kernel<96, 32, 8>", 192: "cnblock_mlp_kernel<192, 16, 4>"}[c]
+
+
+def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor) -> Tensor:
+    """In place on ``x`` [M, C]: x += gamma * (W2 gelu(W1 t + b1) + b2) -- the whole CNBlock MLP
+    of a narrow stage (C = 96 / 192) in one kernel, the hidden activation kept in registers
+    (csrc/mlp_f32.hip)."""
+    for v, what in ((t, "mlp input"), (w1, "fc1 weight"), (b1, "fc1 bias"), (w2, "fc2 weight"), (b2, "fc2 bias"),
+                    (gamma, "layer scale"), (x, "residual")):
+        _chk(v, what)
+    m, c = t.shape
+    if c not in MLP_FUSED_CHANNELS or tuple(x.shape) != (m, c) or tuple(w1.shape) != (4 * c, c) \
+            or tuple(w2.shape) != (c, 4 * c) or b1.numel() != 4 * c or b2.numel() != c or gamma.numel() != c:
+        raise RuntimeError(f"cnblock_mlp: shapes t {tuple(t.shape)} w1 {tuple(w1.shape)} w2 {tuple(w2.shape)}")
+    _launch(cnblock_mlp_kernel_name(c), 2.0 * 2 * m * 4 * c * c,
+            lambda: _lib.call("pipnet_cnblock_mlp_f32", t.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                              b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), m, c, _stream(t)))
+    return x
 
 
 def dwconv7_ln(x_nhwc: Tensor, w_packed: Tensor, bias: Tensor, ln_w: Tensor, ln_b: Tensor,

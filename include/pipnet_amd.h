@@ -233,6 +233,15 @@ int pipnet_layernorm_f32(const float* x, int64_t rows, int C, const float* w, co
 int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
                             float* pooled, void* stream);
 
+/* Fused CNBlock MLP of the narrow ConvNeXt stages (torchvision CNBlock block.3-5 + layer_scale +
+ * residual; the Linear / GELU / Linear of features.1 and features.3):
+ *   x[M,C] += gamma * (W2 gelu_erf(W1 t + b1) + b2)        in place on x
+ * t: [M,C] (dwconv7 + LayerNorm output), W1: [4C,C], b1: [4C], W2: [C,4C], b2 / gamma: [C];
+ * C = 96 or 192; exact fp32 (v_mfma_f32_16x16x4_f32), the 4C-wide hidden activation never
+ * leaves the registers.  All pointers 16-B aligned. */
+int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2, const float* b2,
+                           const float* gamma, float* x, int64_t M, int C, void* stream);
+
 /* NonNegLinear (pipnet.py:54-71, count_pipnet.py:176-224): out = x' relu(W)^T + b with
  * x' = where(x < thresh, 0, x) when apply_thresh (pipnet.py:36, inference) else x.
  * x: [B,D], W: [K,D] read at call time (callers mutate it in place, test.py:73),

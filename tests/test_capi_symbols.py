@@ -66,13 +66,15 @@ def test_argument_validation_without_gpu():
                                   ctypes.c_void_p(16), None) == 1
 
 
-def _kernel_symbols():
+def _nm_demangled():
     import shutil
     import subprocess
     nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
-    out = subprocess.run([nm, "-C", build.LIB],
-                         capture_output=True, text=True, check=True).stdout
-    return set(re.findall(r"void (pipnet_\w+::\w+<.*>)\(", out))     # greedy: nested Cfg<...>
+    return subprocess.run([nm, "-C", build.LIB], capture_output=True, text=True, check=True).stdout
+
+
+def _kernel_symbols():
+    return set(re.findall(r"void (pipnet_\w+::\w+<.*>)\(", _nm_demangled()))     # greedy: nested Cfg<...>
 
 
 def test_roofline_kernel_names_exist_in_library():
@@ -95,6 +97,9 @@ def test_roofline_kernel_names_exist_in_library():
         assert name in syms, (m, n, k, epi, aload, name)
     # split-bf16 ConvNeXt GEMMs (stage-1/2 fc1 / fc2 incl. the N = 96 padded-column tile) and
     # ResNet bf16 convs
+    out = _nm_demangled()
+    for c in K.MLP_FUSED_CHANNELS:         # fused narrow-stage CNBlock MLP (csrc/mlp_f32.hip)
+        assert K.cnblock_mlp_kernel_name(c) in out, c
     for m, n, epi, s3 in [(200704, 96, _lib.EPI_F32_RESID, True), (200704, 384, _lib.EPI_S3_GELU, True),
                           (50176, 192, _lib.EPI_F32_RESID, True), (401408, 64, _lib.EPI_BIAS_RELU, False),
                           (100352, 128, _lib.EPI_BIAS_RELU, False)]:

@@ -248,3 +248,36 @@ def test_linear_splitk(gpu, epi):
     out = K.linear(d(a), d(w), d(b), epi, scale=d(s), r=d(r)).double().cpu()
     tol = 4e-6 * (1 + ref.abs()) + 4e-6 * ((a.abs() @ w.abs().t()) * (1 + s.abs() + r.abs()))
     assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize("c,m", [(96, 1000), (96, 128), (192, 777), (192, 64), (96, 1), (192, 3)])
+def test_cnblock_mlp_fused(gpu, c, m):
+    """The fused narrow-stage CNBlock MLP (csrc/mlp_f32.hip): x + gamma*(W2 gelu(W1 t + b1) + b2)
+    against fp64 torch, ragged M (rows past the last 128-/64-pixel workgroup), asymmetric
+    weights; and against the unfused Linear1+GELU / Linear2+residual kernels (different fp32
+    summation order, so close, not bitwise)."""
+    g = torch.Generator().manual_seed(c + m)
+    t, x = _rand(m, c, gen=g), _rand(m, c, gen=g)
+    w1, b1 = _rand(4 * c, c, gen=g, scale=0.1), _rand(4 * c, gen=g, scale=0.5)
+    w2, b2 = _rand(c, 4 * c, gen=g, scale=0.05), _rand(c, gen=g)
+    gm = _rand(c, gen=g)
+    hid = F.gelu(t @ w1.t() + b1)
+    ref = x + gm * (hid @ w2.t() + b2)
+    d = lambda v: v.float().to(gpu).contiguous()  # noqa: E731
+    xo = d(x)
+    K.cnblock_mlp(d(t), d(w1), d(b1), d(w2), d(b2), d(gm), xo)
+    out = xo.double().cpu()
+    tol = 4e-6 * (gm.abs() * ((hid.abs() @ w2.abs().t()) + (t.abs() @ w1.abs().t()).mean())) + 1e-5
+    assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
+    # the unfused kernels on the same inputs
+    xu = d(x)
+    u = K.linear(d(t), d(w1), d(b1), _lib.EPI_BIAS_GELU)
+    K.linear(u, d(w2), d(b2), _lib.EPI_RESID, scale=d(gm), r=xu, out=xu)
+    assert torch.allclose(xo, xu, rtol=1e-5, atol=1e-5)
+
+
+def test_cnblock_mlp_rejects_unsupported(gpu):
+    z = torch.zeros(4, 384, device=gpu)
+    with pytest.raises(RuntimeError):
+        K.cnblock_mlp(z, torch.zeros(1536, 384, device=gpu), torch.zeros(1536, device=gpu),
+                      torch.zeros(384, 1536, device=gpu), torch.zeros(384, device=gpu), torch.zeros(384, device=gpu), z)

@@ -53,14 +53,16 @@ def main():
         c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         res = {}
         # correctness: the full-line kernel accumulates in the same k order as the 32-deep one
-        if 32 in abls and 0 in abls:
+        for alt in (32, 256):
+            if alt not in abls or 0 not in abls:
+                continue
             c2 = torch.empty_like(c)
             assert lib.lab_pp(0, a.data_ptr(), w.data_ptr(), c.data_ptr(), m, n, k, budgets[0], stream) == 0
-            assert lib.lab_pp(32, a.data_ptr(), w.data_ptr(), c2.data_ptr(), m, n, k, budgets[0], stream) == 0
+            assert lib.lab_pp(alt, a.data_ptr(), w.data_ptr(), c2.data_ptr(), m, n, k, budgets[0], stream) == 0
             torch.cuda.synchronize()
             ref = (a[:512].float() @ w.float().t())
             err = (c[:512].float() - ref).abs().max().item() / ref.abs().max().item()
-            print(f"{name}: p64 == pp bitwise: {torch.equal(c, c2)}; pp vs fp32 matmul (first 512 rows) "
+            print(f"{name}: variant {alt} == pp bitwise: {torch.equal(c, c2)}; pp vs fp32 matmul (first 512 rows) "
                   f"max rel err {err:.2e}", flush=True)
         for _ in range(rounds):
             for abl in abls:
