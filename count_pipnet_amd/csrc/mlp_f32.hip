@@ -28,9 +28,10 @@
 
 namespace {
 
-template <int C, int HC, int NW>
+template <int C, int HC, int NW, int PX = 1>
 struct MlpGeo {
   static constexpr int NT = 64 * NW;
+  static constexpr int PXW = 16 * PX;                                      // pixels per wave
   static constexpr int W1F = HC * C, W2F = C * HC, CHUNK_F = W1F + W2F;   // floats per chunk
   static constexpr int NCH = 4 * C / HC;                                   // hidden chunks
   static constexpr int W1_PIECES = W1F / 256, PIECES = CHUNK_F / 256;      // 1-KiB LDS-DMA pieces
@@ -45,13 +46,14 @@ struct MlpGeo {
   static PIPNET_DEV int f2(int r) { return HC == 32 ? (r & 7) : ((r >> 1) & 3); }
 };
 
-template <int C, int HC, int NW>
+// PX = 16-pixel groups per wave: each W fragment read from LDS feeds PX MFMAs.
+template <int C, int HC, int NW, int PX>
 __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
                                                               const float* __restrict__ W2,
                                                               const float* __restrict__ b2,
                                                               const float* __restrict__ gamma, float* x, int M) {
-  using G = MlpGeo<C, HC, NW>;
+  using G = MlpGeo<C, HC, NW, PX>;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA early): two chunk
   // buffers, then b1 (staged once: a per-chunk global load of it would wait for the DMA)
   __shared__ __attribute__((aligned(16))) float smem[2 * G::CHUNK_F + 4 * C];
@@ -60,8 +62,7 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int q = lane >> 4, pl = lane & 15;
-  const int pix = blockIdx.x * (16 * NW) + 16 * wid + pl;
-  const int prow = pix < M ? pix : M - 1;               // rows past M compute garbage, never stored
+  const int pix0 = blockIdx.x * (G::PXW * NW) + G::PXW * wid + pl;   // pixel of group 0; group u: + 16 u
 
   // ---- LDS-DMA sources of this wave's pieces (chunk 0); chunk c adds c*HC*C (W1) / c*HC (W2) ----
   const float* src[G::PPW];
@@ -95,13 +96,20 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   for (int i = tid; i < C; i += G::NT) st4(sb1 + 4 * i, ld4(b1 + 4 * i));
   stage(0);
 
-  // ---- t of this lane's pixel in registers: tb[g] = t[pix][16 g + 4 q .. + 3] ----
-  f32x4 tb[C / 16];
+  // ---- t of this lane's pixels in registers: tb[u][g] = t[pixel u][16 g + 4 q .. + 3] ----
+  f32x4 tb[PX][C / 16];
 #pragma unroll
-  for (int g = 0; g < C / 16; ++g) tb[g] = ld4(t + (int64_t)prow * C + 16 * g + 4 * q);
-  f32x4 acc[C / 16];
+  for (int u = 0; u < PX; ++u) {
+    const int pix = pix0 + 16 * u;
+    const int prow = pix < M ? pix : M - 1;             // rows past M compute garbage, never stored
 #pragma unroll
-  for (int cb = 0; cb < C / 16; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < C / 16; ++g) tb[u][g] = ld4(t + (int64_t)prow * C + 16 * g + 4 * q);
+  }
+  f32x4 acc[PX][C / 16];
+#pragma unroll
+  for (int u = 0; u < PX; ++u)
+#pragma unroll
+    for (int cb = 0; cb < C / 16; ++cb) acc[u][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // fragment offsets (floats) inside a chunk image
   auto w1_off = [&](int hb, int g) {
@@ -112,69 +120,97 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
     const int r = 16 * cb + pl;
     return G::W1F + r * HC + 4 * ((4 * hb + q) ^ G::f2(r));
   };
+  constexpr int NHB = HC / 16;
 
   for (int ch = 0; ch < G::NCH; ++ch) {
     // this wave's pieces of chunk ch landed, every wave's reads of chunk ch-1 retired
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (ch + 1 < G::NCH) stage(ch + 1);                 // into the buffer of chunk ch-1
     const float* buf = smem + (ch & 1) * G::CHUNK_F;
-    constexpr int NHB = HC / 16;
-    // GEMM1: h^T[16 hb + 4q + i][pixel] for the NHB hidden blocks of the chunk
-    f32x4 h[NHB];
+    // GEMM1: h^T[16 hb + 4q + i][pixel] for the NHB hidden blocks of the chunk; consecutive
+    // MFMAs go to different accumulators (16x16x4: 40-cycle dependent latency, 32-cycle issue)
+    f32x4 h[PX][NHB];
 #pragma unroll
-    for (int hb = 0; hb < NHB; ++hb) h[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < PX; ++u)
+#pragma unroll
+      for (int hb = 0; hb < NHB; ++hb) h[u][hb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int g = 0; g < C / 16; ++g) {
+      f32x4 w[NHB];
 #pragma unroll
-      for (int hb = 0; hb < NHB; ++hb) {
-        const f32x4 w = ld4(buf + w1_off(hb, g));
+      for (int hb = 0; hb < NHB; ++hb) w[hb] = ld4(buf + w1_off(hb, g));
 #pragma unroll
-        for (int s = 0; s < 4; ++s) h[hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s], tb[g][s], h[hb], 0, 0, 0);
-      }
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int hb = 0; hb < NHB; ++hb)
+#pragma unroll
+          for (int u = 0; u < PX; ++u)
+            h[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[hb][s], tb[u][g][s], h[u][hb], 0, 0, 0);
     }
     // + b1, GELU (the unfused Linear1 epilogue's packed form)
 #pragma unroll
     for (int hb = 0; hb < NHB; ++hb) {
       const f32x4 bb = ld4(sb1 + ch * HC + 16 * hb + 4 * q);
-      const f32x4 v = h[hb] + bb;
-      const f32x2 lo = gelu_pk16(f32x2{v[0], v[1]}), hi = gelu_pk16(f32x2{v[2], v[3]});
-      h[hb] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-    }
-    // GEMM2: out^T[c][pixel] += W2[c][hidden] h^T[hidden][pixel]
 #pragma unroll
-    for (int cb = 0; cb < C / 16; ++cb) {
-#pragma unroll
-      for (int hb = 0; hb < NHB; ++hb) {
-        const f32x4 w = ld4(buf + w2_off(cb, hb));
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[s], h[hb][s], acc[cb], 0, 0, 0);
+      for (int u = 0; u < PX; ++u) {
+        const f32x4 v = h[u][hb] + bb;
+        const f32x2 lo = gelu_pk16(f32x2{v[0], v[1]}), hi = gelu_pk16(f32x2{v[2], v[3]});
+        h[u][hb] = f32x4{lo[0], lo[1], hi[0], hi[1]};
       }
+    }
+    // GEMM2: out^T[c][pixel] += W2[c][hidden] h^T[hidden][pixel]; the cb loop innermost, so
+    // consecutive MFMAs go to different accumulators
+#pragma unroll
+    for (int hb = 0; hb < NHB; ++hb) {
+      f32x4 w[C / 16];
+#pragma unroll
+      for (int cb = 0; cb < C / 16; ++cb) w[cb] = ld4(buf + w2_off(cb, hb));
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int cb = 0; cb < C / 16; ++cb)
+#pragma unroll
+          for (int u = 0; u < PX; ++u)
+            acc[u][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cb][s], h[u][hb][s], acc[u][cb], 0, 0, 0);
     }
   }
   // ---- epilogue: x[pixel][c .. c+3] += gamma * (acc + b2), c = 16 cb + 4 q ----
-  if (pix < M) {
-    float* xr = x + (int64_t)pix * C;
 #pragma unroll
-    for (int cb = 0; cb < C / 16; ++cb) {
-      const int c = 16 * cb + 4 * q;
-      const f32x4 r = ld4(xr + c);
-      const f32x4 bb = ld4(b2 + c), gm = ld4(gamma + c);
-      st4(xr + c, r + gm * (acc[cb] + bb));
+  for (int u = 0; u < PX; ++u) {
+    const int pix = pix0 + 16 * u;
+    if (pix < M) {
+      float* xr = x + (int64_t)pix * C;
+#pragma unroll
+      for (int cb = 0; cb < C / 16; ++cb) {
+        const int c = 16 * cb + 4 * q;
+        const f32x4 r = ld4(xr + c);
+        const f32x4 bb = ld4(b2 + c), gm = ld4(gamma + c);
+        st4(xr + c, r + gm * (acc[u][cb] + bb));
+      }
     }
   }
 }
 
-template <int C, int HC, int NW>
+template <int C, int HC, int NW, int PX>
 int launch_mlp(const float* t, const float* W1, const float* b1, const float* W2, const float* b2, const float* gamma,
                float* x, int M, hipStream_t s) {
-  const int px = 16 * NW;
-  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1, b1, W2,
-                     b2, gamma, x, M);
+  const int px = 16 * PX * NW;
+  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1, b1,
+                     W2, b2, gamma, x, M);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }
 
+// Instantiations chosen with tools/mlp_lab.py (profiles/r02/mlp_lab.txt).  The per-pixel
+// arithmetic does not depend on them (the hidden index is summed in 16-blocks in order for
+// any HC), so the M-dependent choice keeps results batch-invariant.
+
 }  // namespace
+
+#ifdef PIPNET_MLP_LAB
+bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float* b1, const float* W2, const float* b2,
+                            const float* gamma, float* x, int M, hipStream_t s);
+#endif
 
 extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2,
                                       const float* b2, const float* gamma, float* x, int64_t M, int C,
@@ -186,6 +222,10 @@ extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const flo
     return PIPNET_ERR_ALIGN;
   if (M == 0) return PIPNET_OK;
   hipStream_t s = (hipStream_t)stream;
-  if (C == 96) return launch_mlp<96, 32, 8>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
-  return launch_mlp<192, 16, 4>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
+#ifdef PIPNET_MLP_LAB
+  if (pipnet_mlp_lab_variant(C, t, W1, b1, W2, b2, gamma, x, (int)M, s)) return PIPNET_OK;
+#endif
+  if (C == 96) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
+  if (M >= 32768) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);   // C2 stage 2
+  return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);                  // C5 stage 2
 }

@@ -329,8 +329,11 @@ def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tens
 MLP_FUSED_CHANNELS = (96, 192)
 
 
-def cnblock_mlp_kernel_name(c: int) -> str:
-    return {96: "cnblock_mlp_kernel<96, 32, 8>", 192: "cnblock_mlp_kernel<192, 16, 4>"}[c]
+def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20) -> str:
+    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_f32)."""
+    if c == 96:
+        return "cnblock_mlp_kernel<96, 32, 8, 1>"
+    return "cnblock_mlp_kernel<192, 16, 8, 1>" if m >= 32768 else "cnblock_mlp_kernel<192, 32, 4, 1>"
 
 
 def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor) -> Tensor:
@@ -344,7 +347,7 @@ def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma
     if c not in MLP_FUSED_CHANNELS or tuple(x.shape) != (m, c) or tuple(w1.shape) != (4 * c, c) \
             or tuple(w2.shape) != (c, 4 * c) or b1.numel() != 4 * c or b2.numel() != c or gamma.numel() != c:
         raise RuntimeError(f"cnblock_mlp: shapes t {tuple(t.shape)} w1 {tuple(w1.shape)} w2 {tuple(w2.shape)}")
-    _launch(cnblock_mlp_kernel_name(c), 2.0 * 2 * m * 4 * c * c,
+    _launch(cnblock_mlp_kernel_name(c, m), 2.0 * 2 * m * 4 * c * c,
             lambda: _lib.call("pipnet_cnblock_mlp_f32", t.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
                               b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), m, c, _stream(t)))
     return x

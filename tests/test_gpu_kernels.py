@@ -250,7 +250,7 @@ def test_linear_splitk(gpu, epi):
     assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
 
 
-@pytest.mark.parametrize("c,m", [(96, 1000), (96, 128), (192, 777), (192, 64), (96, 1), (192, 3)])
+@pytest.mark.parametrize("c,m", [(96, 1000), (96, 128), (192, 777), (192, 64), (96, 1), (192, 3), (192, 40000)])
 def test_cnblock_mlp_fused(gpu, c, m):
     """The fused narrow-stage CNBlock MLP (csrc/mlp_f32.hip): x + gamma*(W2 gelu(W1 t + b1) + b2)
     against fp64 torch, ragged M (rows past the last 128-/64-pixel workgroup), asymmetric

@@ -1,0 +1,20 @@
+// Tuning lab for the fused narrow-stage CNBlock MLP (not part of the product library): the
+// product kernel (count_pipnet_amd/csrc/mlp_f32.hip) with other (HC, waves, pixel groups)
+// instantiations selected by mlp_lab_set().  Built by tools/mlp_lab.py.
+#define PIPNET_MLP_LAB
+#include "../count_pipnet_amd/csrc/mlp_f32.hip"
+
+static int g_variant = 0;
+extern "C" void mlp_lab_set(int v) { g_variant = v; }
+
+bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float* b1, const float* W2, const float* b2,
+                            const float* gamma, float* x, int M, hipStream_t s) {
+#define V(ID, CC, HC, NW, PX) \
+  case ID: if (C != CC) return false; launch_mlp<CC, HC, NW, PX>(t, W1, b1, W2, b2, gamma, x, M, s); return true;
+  switch (g_variant) {
+    V(1, 96, 32, 8, 2) V(2, 96, 32, 4, 2) V(4, 96, 32, 4, 1) V(5, 96, 16, 4, 2)
+    V(11, 192, 32, 8, 1) V(12, 192, 32, 4, 1) V(13, 192, 16, 8, 1) V(14, 192, 16, 2, 1)
+    default: return false;
+  }
+#undef V
+}
