@@ -225,7 +225,16 @@ extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const flo
 #ifdef PIPNET_MLP_LAB
   if (pipnet_mlp_lab_variant(C, t, W1, b1, W2, b2, gamma, x, (int)M, s)) return PIPNET_OK;
 #endif
-  if (C == 96) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);
-  if (M >= 32768) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);   // C2 stage 2
-  return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, (int)M, s);                  // C5 stage 2
+  // small M (C1: 16 images of 64^2) gets smaller workgroups so that the grid still covers the CUs
+  const int m = (int)M;
+  if (C == 96) {
+    if (m >= 65536) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C2 / C5 stage 1
+    if (m >= 16384) return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    if (m >= 8192) return launch_mlp<96, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    return launch_mlp<96, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+  }
+  if (m >= 32768) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);      // C2 stage 2
+  if (m >= 8192) return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);       // C5 stage 2
+  if (m >= 4096) return launch_mlp<192, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+  return launch_mlp<192, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
 }

@@ -98,7 +98,8 @@ def test_roofline_kernel_names_exist_in_library():
     # split-bf16 ConvNeXt GEMMs (stage-1/2 fc1 / fc2 incl. the N = 96 padded-column tile) and
     # ResNet bf16 convs
     out = _nm_demangled()
-    for c, m in [(96, 200704), (192, 50176), (192, 16384)]:    # fused narrow-stage MLP (csrc/mlp_f32.hip)
+    for c, m in [(96, 200704), (96, 20000), (96, 9000), (96, 4096), (192, 50176), (192, 16384), (192, 5000),
+                 (192, 1024)]:                                 # fused narrow-stage MLP (csrc/mlp_f32.hip)
         assert K.cnblock_mlp_kernel_name(c, m) in out, (c, m)
     for m, n, epi, s3 in [(200704, 96, _lib.EPI_F32_RESID, True), (200704, 384, _lib.EPI_S3_GELU, True),
                           (50176, 192, _lib.EPI_F32_RESID, True), (401408, 64, _lib.EPI_BIAS_RELU, False),

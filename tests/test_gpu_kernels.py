@@ -281,3 +281,23 @@ def test_cnblock_mlp_rejects_unsupported(gpu):
     with pytest.raises(RuntimeError):
         K.cnblock_mlp(z, torch.zeros(1536, 384, device=gpu), torch.zeros(1536, device=gpu),
                       torch.zeros(384, 1536, device=gpu), torch.zeros(384, device=gpu), torch.zeros(384, device=gpu), z)
+
+
+@pytest.mark.parametrize("c,m", [(96, 70000), (192, 40000)])
+def test_cnblock_mlp_batch_invariant(gpu, c, m):
+    """The launch configuration of the fused MLP depends on M (workgroup size), its per-pixel
+    arithmetic must not: every instantiation gives the same bits for a pixel."""
+    g = torch.Generator(device=gpu).manual_seed(c)
+    t = torch.randn(m, c, device=gpu, generator=g)
+    x = torch.randn(m, c, device=gpu, generator=g)
+    w1 = torch.randn(4 * c, c, device=gpu, generator=g) * 0.1
+    b1 = torch.randn(4 * c, device=gpu, generator=g)
+    w2 = torch.randn(c, 4 * c, device=gpu, generator=g) * 0.05
+    b2 = torch.randn(c, device=gpu, generator=g)
+    gm = torch.randn(c, device=gpu, generator=g)
+    full = x.clone()
+    K.cnblock_mlp(t, w1, b1, w2, b2, gm, full)
+    for rows in (20000, 9000, 4096, 1000, 17):
+        part = x[:rows].clone()
+        K.cnblock_mlp(t[:rows].contiguous(), w1, b1, w2, b2, gm, part)
+        assert torch.equal(part, full[:rows]), rows
