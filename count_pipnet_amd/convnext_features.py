@@ -237,9 +237,10 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
 FUSED_MLP = True      # tools / A-B runs may switch the fused narrow-stage MLP off
 # The fused MLP parallelises over pixels only (16 per wave): on small feature maps (C1's 64^2
 # inputs: 256 / 64 pixels per image) the unfused GEMMs, which also spread the hidden dimension
-# over workgroups, are faster.  The choice depends on the layer's h*w, never on the batch size,
-# so per-pixel results stay batch-invariant.
-MLP_FUSED_MIN_PIXELS = 512
+# over workgroups, are faster.  The choice depends on the layer's C and h*w, never on the batch
+# size, so per-pixel results stay batch-invariant.  (C = 192 at 16^2, C5's stage 2: fused
+# ~100 us vs 115 unfused per block at batch 64, tools/ab_mlp.py.)
+MLP_FUSED_MIN_PIXELS = {96: 512, 192: 256}
 
 
 def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Optional[Tensor] = None) -> Tensor:
@@ -255,7 +256,8 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
     wdw = packed(cache, key + ".dw", dw.weight, lambda w: w.reshape(c, 49).t())
     t = K.dwconv7_ln(h, wdw, dw.bias, ln.weight, ln.bias)
     hv = h.view(-1, c)
-    if row_scale is None and c in K.MLP_FUSED_CHANNELS and FUSED_MLP and hh * ww >= MLP_FUSED_MIN_PIXELS:
+    if row_scale is None and c in K.MLP_FUSED_CHANNELS and FUSED_MLP \
+            and hh * ww >= MLP_FUSED_MIN_PIXELS[c]:
         # narrow stages: Linear1 + GELU + Linear2 + layer_scale + residual in one kernel
         K.cnblock_mlp(t.view(-1, c), l1.weight, l1.bias, l2.weight, l2.bias, blk.layer_scale.view(-1), hv)
         return h

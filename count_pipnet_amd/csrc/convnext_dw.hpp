@@ -7,6 +7,68 @@ namespace pipnet_dw {
 constexpr float LN_EPS = 1e-6f;
 constexpr int DW_THREADS = 192;
 
+// LayerNorm + store of npix buffered pixels (LDS, C floats each, row-major NP per output
+// row): C/12 lanes per pixel, each owning 3 float4 channel chunks (sl, sl + C/12, sl + C/6),
+// so one store instruction writes C/12 * 16 B contiguous of a pixel (a full 128 B line at
+// C = 96); gamma / beta stay in registers; two-pass mean / variance as torch.
+template <int C, bool S3>
+__device__ __forceinline__ void ln_rows_vec(const float* tile, int npix, int NP, int b, int H, int W, int oy0,
+                                            int xblk, const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                            void* __restrict__ yv) {
+  constexpr int LPP = C / 12, PPW = 64 / LPP;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sub = lane / LPP, sl = lane % LPP;
+  f32x4 g[3], be[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    g[j] = ld4(lnw + 4 * (sl + LPP * j));
+    be[j] = ld4(lnb + 4 * (sl + LPP * j));
+  }
+  for (int base = wv * PPW; base < npix; base += nw * PPW) {
+    const int pp = base + sub;
+    const int t = pp / NP, pix = pp - t * NP;
+    const int ox = xblk + pix, oy = oy0 + t;
+    const bool ok = pp < npix && ox < W && oy < H;
+    f32x4 v[3];
+    float sm = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      v[j] = ok ? ld4(tile + pp * C + 4 * (sl + LPP * j)) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+    }
+#pragma unroll
+    for (int o = LPP / 2; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
+    const float mean = sm * (1.0f / C);
+    float qq = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      v[j] -= mean;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) qq = fmaf(v[j][e], v[j][e], qq);
+    }
+#pragma unroll
+    for (int o = LPP / 2; o > 0; o >>= 1) qq += __shfl_xor(qq, o, 64);
+    const float rstd = 1.0f / sqrtf(qq * (1.0f / C) + LN_EPS);
+    if (!ok) continue;
+    const int64_t opix = ((int64_t)b * H + oy) * W + ox;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const f32x4 r = v[j] * rstd * g[j] + be[j];
+      const int c = 4 * (sl + LPP * j);
+      if constexpr (S3) {
+        __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 2 * C + c;
+        __bf16 hi[4], lo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) split_bf16(r[e], hi[e], lo[e]);
+        *reinterpret_cast<uint2*>(dst) = *reinterpret_cast<const uint2*>(hi);
+        *reinterpret_cast<uint2*>(dst + C) = *reinterpret_cast<const uint2*>(lo);
+      } else {
+        st4(reinterpret_cast<float*>(yv) + opix * C + c, r);
+      }
+    }
+  }
+}
+
 // 192 threads = G groups x (C/4) channel quads; group g computes a TY x TX tile of output
 // pixels (TY rows, TX consecutive columns).  Each input row of the 7-row halo is loaded
 // once into registers (TX+6 float4) and feeds every output row it touches; the raw tile
@@ -73,6 +135,10 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
     for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
   __syncthreads();
 
+  if constexpr (LPP * 12 == C) {
+    ln_rows_vec<C, S3>(tile, TY * NP, NP, b, H, W, oy0, xblk, lnw, lnb, yv);
+    return;
+  }
   // LayerNorm: LPP lanes per pixel (64 / LPP pixels per wave at once, log2(LPP)-step
   // shuffle reductions -- one pixel per wave (LPP = 64) serialised two 6-step reductions
   // per pixel); two-pass mean / variance as torch

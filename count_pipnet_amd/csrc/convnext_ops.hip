@@ -200,18 +200,21 @@ extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, con
   return PIPNET_OK;
 }
 
-// LayerNorm lanes per pixel (tools/dw_lab.hip, profiles/r01/dw_lab_lpp.txt): 16 for C = 96 / 192
-// (98 -> 70 us, 44 -> 38 us at C2), 32 for 384, 64 for 768 (no difference there).
+// LayerNorm lanes per pixel = C / 12: each lane owns 3 float4 channel chunks, gamma / beta in
+// registers, full-line stores (tools/dw_lab.hip, profiles/r02/dw_lab.txt: 64 -> 63 / 37 -> 35 /
+// 59 -> 56 / 90 -> 85 us at the C2 stages).
 extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C, const float* w_packed,
                                      const float* bias, const float* ln_w, const float* ln_b, float* y,
                                      void* stream) {
   if (B < 0 || H <= 0 || W <= 0) return PIPNET_ERR_ARG;
   if (!x || !w_packed || !bias || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
-  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias)) return PIPNET_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias) || !aligned16(ln_w) || !aligned16(ln_b) ||
+      !aligned16(y))
+    return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
-    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192: return pipnet_dw::launch_dw<192, 7, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, false, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
@@ -223,11 +226,13 @@ extern "C" int pipnet_dwconv7_ln_s3(const float* x, int B, int H, int W, int C, 
                                     const float* bias, const float* ln_w, const float* ln_b, void* y, void* stream) {
   if (B < 0 || H <= 0 || W <= 0) return PIPNET_ERR_ARG;
   if (!x || !w_packed || !bias || !ln_w || !ln_b || !y) return PIPNET_ERR_ARG;
-  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias)) return PIPNET_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(bias) || !aligned16(ln_w) || !aligned16(ln_b) ||
+      !aligned16(y))
+    return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
-    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 96: return pipnet_dw::launch_dw<96, 7, 1, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192: return pipnet_dw::launch_dw<192, 7, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, true, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);

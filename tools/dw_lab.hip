@@ -1,17 +1,36 @@
-// Tuning lab for the depthwise 7x7 + LayerNorm kernel (not part of the product ABI).
+// Tuning lab for the depthwise 7x7 + LayerNorm kernel (not part of the product ABI):
+// v0 = the register-tile kernel (convnext_dw.hpp), v1.. = row-ring variants (convnext_dw_ring.hpp).
 #include "../count_pipnet_amd/csrc/convnext_dw.hpp"
+#include "../count_pipnet_amd/csrc/convnext_dw_ring.hpp"
 using namespace pipnet_dw;
 
 extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, const float* wp, const float* bias,
-                      const float* lnw, const float* lnb, float* y, void* stream) {
+                      const float* lnw, const float* lnb, float* y, void* stream, int min_wg, int min_rh) {
   hipStream_t s = (hipStream_t)stream;
 #define V(ID, CC, TX, TY, MB, LPP) \
   if (variant == ID && C == CC) return launch_dw<CC, TX, TY, MB, false, LPP>(x, B, H, W, wp, bias, lnw, lnb, y, s);
-  // v0 = the product's choice (LPP 64); v1-v4: lanes per LayerNorm pixel 32 / 16, TY 1 / 2
-  V(0, 96, 7, 1, 1, 64) V(1, 96, 7, 1, 1, 32) V(2, 96, 7, 1, 1, 16) V(3, 96, 7, 2, 1, 16) V(4, 96, 14, 1, 1, 16)
-  V(0, 192, 7, 1, 1, 64) V(1, 192, 7, 1, 1, 32) V(2, 192, 7, 1, 1, 16) V(3, 192, 7, 2, 1, 16) V(4, 192, 14, 1, 1, 16)
-  V(0, 384, 7, 1, 2, 64) V(1, 384, 7, 1, 2, 32) V(2, 384, 7, 1, 2, 16) V(3, 384, 14, 1, 1, 16) V(4, 384, 7, 2, 2, 16)
-  V(0, 768, 13, 1, 1, 64) V(1, 768, 13, 1, 1, 32) V(2, 768, 13, 1, 1, 16) V(3, 768, 7, 1, 2, 16) V(4, 768, 7, 1, 2, 32)
+#define R(ID, CC, TX, NS, MB, LPP)                                                                                 \
+  if (variant == ID && C == CC)                                                                                     \
+    return launch_dw_ring<CC, TX, NS, MB, false, LPP>(x, B, H, W, wp, bias, lnw, lnb, y, s, min_wg, min_rh);
+  V(0, 96, 7, 1, 1, 16) V(0, 192, 7, 1, 1, 16) V(0, 384, 7, 1, 2, 32) V(0, 768, 13, 1, 1, 64)
+  // v5-v7: tile kernel with the vectorised LayerNorm (LPP = C / 12) at other tiles
+  V(5, 96, 7, 1, 1, 8) V(5, 192, 7, 1, 1, 16) V(5, 384, 7, 1, 2, 32) V(5, 768, 13, 1, 1, 64)
+  V(6, 96, 7, 1, 2, 8) V(6, 192, 7, 1, 2, 16) V(6, 384, 14, 1, 1, 32) V(6, 768, 7, 1, 2, 64)
+  V(7, 96, 14, 1, 1, 8) V(7, 192, 14, 1, 1, 16) V(7, 384, 7, 2, 1, 32) V(7, 768, 13, 1, 2, 64)
+  R(1, 96, 4, 4, 2, 16) R(2, 96, 2, 4, 3, 16) R(3, 96, 4, 8, 1, 16) R(4, 96, 3, 4, 2, 16)
+  R(1, 192, 4, 2, 2, 16) R(2, 192, 2, 2, 3, 16) R(3, 192, 4, 4, 1, 16) R(4, 192, 3, 2, 2, 16)
+  R(1, 384, 4, 1, 2, 32) R(2, 384, 2, 1, 3, 32) R(3, 384, 4, 2, 1, 32) R(4, 384, 3, 1, 2, 32)
+  R(1, 768, 2, 1, 1, 64) R(2, 768, 4, 1, 1, 64) R(3, 768, 2, 1, 1, 32) R(4, 768, 3, 1, 1, 64)
+  // ablations of v1 (ABL bits: 1 no LayerNorm, 2 no FMAs, 4 no input loads)
+#define A(ID, CC, TX, NS, MB, LPP, ABL)                                                                            \
+  if (variant == ID && C == CC)                                                                                     \
+    return launch_dw_ring<CC, TX, NS, MB, false, LPP, ABL>(x, B, H, W, wp, bias, lnw, lnb, y, s, min_wg, min_rh);
+  A(11, 96, 4, 4, 2, 16, 1) A(12, 96, 4, 4, 2, 16, 2) A(14, 96, 4, 4, 2, 16, 4) A(13, 96, 4, 4, 2, 16, 3)
+  A(16, 96, 4, 4, 2, 16, 6)
+  A(11, 384, 4, 1, 2, 32, 1) A(12, 384, 4, 1, 2, 32, 2) A(14, 384, 4, 1, 2, 32, 4) A(13, 384, 4, 1, 2, 32, 3)
+  A(16, 384, 4, 1, 2, 32, 6)
+#undef A
 #undef V
+#undef R
   return 1;
 }

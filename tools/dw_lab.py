@@ -1,43 +1,77 @@
-"""A/B the dwconv7+LN variants of tools/dw_lab.hip on the network's stage shapes."""
+"""A/B the dwconv7+LN variants of tools/dw_lab.hip on the network's stage shapes (C2 224^2
+and C5 128^2 inputs, batch 64): v0 = register-tile kernel, v1.. = row-ring variants, each
+at a few (min workgroups, min rows per chunk) chunkings.  Prints us and HBM-algorithmic
+TB/s (input read + output write once)."""
 import ctypes
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 lib = ctypes.CDLL(os.path.join(HERE, "libdw_lab.so"))
 P, I32 = ctypes.c_void_p, ctypes.c_int
-lib.lab_dw.argtypes = [I32, P, I32, I32, I32, I32, P, P, P, P, P, P]
+lib.lab_dw.argtypes = [I32, P, I32, I32, I32, I32, P, P, P, P, P, P, I32, I32]
 
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream().cuda_stream
-for c, hw in [(96, 56), (192, 28), (384, 27), (768, 26)]:
+CHUNKS = [(2048, 7), (1024, 7), (4096, 4), (512, 14)]
+for c, hw in [(96, 56), (192, 28), (384, 27), (768, 26), (96, 32), (192, 16)]:
     x = torch.randn(64, hw, hw, c, device=dev)
     w = torch.randn(49, c, device=dev) * 0.2
     b, lw, lb = torch.randn(c, device=dev), torch.randn(c, device=dev), torch.randn(c, device=dev)
     y = torch.empty_like(x)
     ref = None
     res = {}
+    combos = [(0, 2048, 7), (5, 2048, 7), (6, 2048, 7), (7, 2048, 7)] + [(v, mw, mr) for v in (1, 3) for mw, mr in CHUNKS[:2]]
     for rnd in range(3):
-        for v in range(5):
+        for v, mw, mr in combos:
             args = (v, x.data_ptr(), 64, hw, hw, c, w.data_ptr(), b.data_ptr(), lw.data_ptr(), lb.data_ptr(),
-                    y.data_ptr(), stream)
+                    y.data_ptr(), stream, mw, mr)
+            y.fill_(float("nan"))
             assert lib.lab_dw(*args) == 0
+            if rnd == 0:
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = y.clone()
+                else:
+                    err = (y - ref).abs().max().item()
+                    assert err < 1e-3, (c, hw, v, mw, mr, err)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
                 lib.lab_dw(*args)
             e1.record()
             torch.cuda.synchronize()
-            res.setdefault(v, []).append(e0.elapsed_time(e1) / 10 * 1e3)
-            if rnd == 0:
-                if ref is None:
-                    ref = y.clone()
-                else:
-                    assert (y - ref).abs().max().item() < 1e-3, (c, v)
+            res.setdefault((v, mw, mr), []).append(e0.elapsed_time(e1) / 10 * 1e3)
     gb = 2 * x.numel() * 4 / 1e9
-    print(f"C={c:4d} " + " ".join(f"v{v}:{min(t):7.1f}us({gb / min(t) * 1e6 / 1e3:4.2f}TB/s)" for v, t in res.items()),
-          flush=True)
+    items = sorted(res.items(), key=lambda kv: min(kv[1]))
+    print(f"C={c:4d} H=W={hw}: v0 {min(res[(0, 2048, 7)]):7.1f}us  best: " +
+          " ".join(f"v{v}/{mw}/{mr}:{min(t):6.1f}us({gb / min(t) * 1e6 / 1e3:4.2f}TB/s)"
+                   for (v, mw, mr), t in items[:6]), flush=True)
+
+# ablations of v1 (no LN / no FMAs / no loads) at the C2 stage-1 and stage-3 shapes
+if "--abl" in sys.argv:
+    for c, hw in [(96, 56), (384, 27)]:
+        x = torch.randn(64, hw, hw, c, device=dev)
+        w = torch.randn(49, c, device=dev) * 0.2
+        b, lw, lb = torch.randn(c, device=dev), torch.randn(c, device=dev), torch.randn(c, device=dev)
+        y = torch.empty_like(x)
+        out = []
+        for v in (1, 11, 12, 14, 13, 16):
+            args = (v, x.data_ptr(), 64, hw, hw, c, w.data_ptr(), b.data_ptr(), lw.data_ptr(), lb.data_ptr(),
+                    y.data_ptr(), stream, 2048, 7)
+            assert lib.lab_dw(*args) == 0
+            ts = []
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    lib.lab_dw(*args)
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1) / 10 * 1e3)
+            out.append(f"v{v}:{min(ts):6.1f}us")
+        print(f"ablation C={c} ({'full', 'noLN', 'noFMA', 'noLoad', 'noLN+noFMA', 'noFMA+noLoad'}): " + " ".join(out),
+              flush=True)
