@@ -70,7 +70,7 @@ SIGNATURES = {
     "pipnet_wgrad_workspace_bytes": [I32, I32, I32],
     "pipnet_wgrad_f32": [P, I64, P, I64, I32, I32, I32, P, I64, I32, P, P],
     "pipnet_wgrad_conv2x2_f32": [P, P, I32, I32, I32, I32, I32, I32, P, I32, P, P],
-    "pipnet_wgrad_conv_f32": [P, P, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
+    "pipnet_wgrad_conv_f32": [P, P, I32, I32, I32, I32, I32, I32, I32, I32, I32, P, I32, P, P],
     "pipnet_colsum_workspace_bytes": [I32],
     "pipnet_colsum_f32": [P, I64, I32, I32, P, I32, P, P],
     "pipnet_train_partials_floats": [I32],
@@ -82,8 +82,14 @@ SIGNATURES = {
     "pipnet_dwconv7_wgrad_f32": [P, P, I32, I32, I32, I32, P, P, I32, P, P],
     "pipnet_head_bwd_f32": [P, P, I32, I32, I32, P, P, I32, F32, F32, F32, P, P, P, P],
     "pipnet_cnblock_mlp_f32": [P, P, P, P, P, P, P, I64, I32, P],
+    "pipnet_bn_workspace_floats": [I32],
+    "pipnet_bn_stats_f32": [P, I64, I32, F32, F32, P, P, P, P, P, P],
+    "pipnet_bn_apply_f32": [P, I64, I32, P, P, P, P, P, I32, P, P],
+    "pipnet_bn_backward_f32": [P, P, P, I64, I32, P, P, P, P, P, P, P, P, P],
+    "pipnet_stride_scatter_f32": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P],
 }
-_RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64}
+_RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64,
+                  "pipnet_bn_workspace_floats": ctypes.c_int64}
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, "pipnet_amd_source_digest": ctypes.c_char_p,
             **_RESTYPE_EXTRA}
 

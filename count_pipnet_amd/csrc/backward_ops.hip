@@ -18,11 +18,12 @@ constexpr int WG_T = 256, WB1 = 128, WB2 = 128, WBK = 32, WPAD = 4;
 constexpr int WLD1 = WB1 + WPAD, WLD2 = WB2 + WPAD;    // padded rows: the two half-waves
                                                          // (k and k+1) hit different banks
 
-// B operand gather of a KHxKW (stride s, no padding) conv's weight gradient -- the 2x2
-// downsample convs and the 4x4/4 stem: row m = output pixel (b, oy, ox), column k =
-// tap * Cin + ci -> input x[b][oy*s + tap/KW][ox*s + tap%KW][ci].
+// B operand gather of a KHxKW (stride s, zero padding p) conv's weight gradient -- the 2x2
+// downsample convs, the 4x4/4 ConvNeXt stem and the ResNet 3x3 / strided 1x1 convs: row m =
+// output pixel (b, oy, ox), column k = tap * Cin + ci -> input x[b][oy*s - p + tap/KW]
+// [ox*s - p + tap%KW][ci] (zero outside the image).
 struct Conv2x2Geom {
-  int H, W, Cin, OH, OW, stride, KW;
+  int H, W, Cin, OH, OW, stride, KW, pad;
 };
 
 template <int BCONV>
@@ -40,10 +41,12 @@ __global__ __launch_bounds__(WG_T, 2) void wgrad_kernel(const float* __restrict_
   const int ntiles = m_end > m_beg ? (m_end - m_beg + WBK - 1) / WBK : 0;
   const int lr = tid >> 5, lc = 4 * (tid & 31);      // loader: rows lr + 8q, columns lc..lc+3
   const bool a_ok = n1_0 + lc < N1, b_ok = n2_0 + lc < N2;
-  int64_t b_tap_off = 0;                              // conv gather: this thread's tap / channel
+  int t_ky = 0, t_kx = 0, t_ci = 0;                   // conv gather: this thread's tap / channel
   if (BCONV) {
-    const int k = n2_0 + lc, tap = k / cg.Cin, ci = k - tap * cg.Cin;
-    b_tap_off = ((int64_t)(tap / cg.KW) * cg.W + (tap % cg.KW)) * cg.Cin + ci;
+    const int k = n2_0 + lc, tap = k / cg.Cin;
+    t_ci = k - tap * cg.Cin;
+    t_ky = tap / cg.KW - cg.pad;
+    t_kx = tap % cg.KW - cg.pad;
   }
   f32x4 ra[4], rb[4];
   auto gload = [&](int m0) {
@@ -55,8 +58,10 @@ __global__ __launch_bounds__(WG_T, 2) void wgrad_kernel(const float* __restrict_
       if (BCONV) {
         const int mm = mok ? m : 0, ohw = cg.OH * cg.OW;
         const int b = mm / ohw, r = mm - b * ohw, oy = r / cg.OW, ox = r - oy * cg.OW;
-        const float* src = B + (((int64_t)b * cg.H + oy * cg.stride) * cg.W + ox * cg.stride) * cg.Cin + b_tap_off;
-        rb[q] = (mok && b_ok) ? ld4(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const int iy = oy * cg.stride + t_ky, ix = ox * cg.stride + t_kx;
+        const bool in = (unsigned)iy < (unsigned)cg.H && (unsigned)ix < (unsigned)cg.W;
+        const float* src = B + (((int64_t)b * cg.H + (in ? iy : 0)) * cg.W + (in ? ix : 0)) * cg.Cin + t_ci;
+        rb[q] = (mok && b_ok && in) ? ld4(src) : f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
         rb[q] = (mok && b_ok) ? ld4(B + (int64_t)m * ldb + n2_0 + lc) : f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -180,7 +185,7 @@ int wgrad_launch(const float* A, int64_t lda, const float* B, int64_t ldb, int M
   if (!direct && !workspace) return PIPNET_ERR_ARG;
   float* out = direct ? C : workspace;
   const int64_t ldo = direct ? ldc : N2;
-  const Conv2x2Geom g = cg ? *cg : Conv2x2Geom{0, 0, 1, 0, 0, 1, 1};
+  const Conv2x2Geom g = cg ? *cg : Conv2x2Geom{0, 0, 1, 0, 0, 1, 1, 0};
   if (cg)
     hipLaunchKernelGGL(wgrad_kernel<1>, dim3((unsigned)tiles, (unsigned)splits), dim3(WG_T), 0, s, A, lda, B, ldb, M,
                        N1, N2, mchunk, t2n, out, ldo, (int64_t)N1 * N2, g);
@@ -214,22 +219,22 @@ extern "C" int pipnet_wgrad_conv2x2_f32(const float* dY, const float* x, int B, 
   if (!dY || !x || !dW) return PIPNET_ERR_ARG;
   if (!aligned16(dY) || !aligned16(x)) return PIPNET_ERR_ALIGN;
   const int OH = (H - 2) / stride + 1, OW = (W - 2) / stride + 1;
-  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, 2};
+  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, 2, 0};
   return wgrad_launch(dY, Cout, x, 4 * Cin, B * OH * OW, Cout, 4 * Cin, dW, 4 * Cin, accumulate, workspace,
                       (hipStream_t)stream, &g);
 }
 
 extern "C" int pipnet_wgrad_conv_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int KH, int KW,
-                                     int stride, int Cout, float* dW, int accumulate, float* workspace,
+                                     int stride, int pad, int Cout, float* dW, int accumulate, float* workspace,
                                      void* stream) {
-  if (B <= 0 || KH <= 0 || KW <= 0 || H < KH || W < KW || Cin <= 0 || Cout <= 0 || (Cin & 3) || (Cout & 3) ||
-      stride <= 0)
+  if (B <= 0 || KH <= 0 || KW <= 0 || pad < 0 || pad >= KH || pad >= KW || H + 2 * pad < KH || W + 2 * pad < KW ||
+      Cin <= 0 || Cout <= 0 || (Cin & 3) || (Cout & 3) || stride <= 0)
     return PIPNET_ERR_ARG;
   if (!dY || !x || !dW) return PIPNET_ERR_ARG;
   if (!aligned16(dY) || !aligned16(x)) return PIPNET_ERR_ALIGN;
-  const int OH = (H - KH) / stride + 1, OW = (W - KW) / stride + 1;
+  const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   const int K = KH * KW * Cin;
-  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, KW};
+  const Conv2x2Geom g{H, W, Cin, OH, OW, stride, KW, pad};
   return wgrad_launch(dY, Cout, x, K, B * OH * OW, Cout, K, dW, K, accumulate, workspace, (hipStream_t)stream, &g);
 }
 

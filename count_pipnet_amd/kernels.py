@@ -915,18 +915,18 @@ def dwconv7_wgrad(dz_nhwc: Tensor, x_nhwc: Tensor, dw_packed: Tensor, db: Tensor
 
 
 def wgrad_conv(dy_nhwc: Tensor, x_nhwc: Tensor, kh: int, kw: int, stride: int, out: Tensor,
-               accumulate: bool = False) -> Tensor:
-    """Packed [Cout, KH*KW*Cin] weight gradient of a KHxKW conv (stride, no padding)."""
+               accumulate: bool = False, pad: int = 0) -> Tensor:
+    """Packed [Cout, KH*KW*Cin] weight gradient of a KHxKW conv (stride, zero padding)."""
     _chk(dy_nhwc, "d conv output")
     _chk(x_nhwc, "conv input")
     b, h, w, cin = x_nhwc.shape
     cout = dy_nhwc.shape[-1]
-    oh, ow = (h - kh) // stride + 1, (w - kw) // stride + 1
+    oh, ow = (h + 2 * pad - kh) // stride + 1, (w + 2 * pad - kw) // stride + 1
     if tuple(dy_nhwc.shape) != (b, oh, ow, cout) or out.numel() != cout * kh * kw * cin:
         raise RuntimeError(f"wgrad_conv: dY {tuple(dy_nhwc.shape)}, x {tuple(x_nhwc.shape)}, k{kh}x{kw}/{stride}")
     nbytes = _lib.load().pipnet_wgrad_workspace_bytes(b * oh * ow, cout, kh * kw * cin)
     ws = torch.empty(max(nbytes // 4, 1), device=x_nhwc.device, dtype=torch.float32)
-    _lib.call("pipnet_wgrad_conv_f32", dy_nhwc.data_ptr(), x_nhwc.data_ptr(), b, h, w, cin, kh, kw, stride, cout,
+    _lib.call("pipnet_wgrad_conv_f32", dy_nhwc.data_ptr(), x_nhwc.data_ptr(), b, h, w, cin, kh, kw, stride, pad, cout,
               out.data_ptr(), int(accumulate), ws.data_ptr(), _stream(x_nhwc))
     return out
 
@@ -956,3 +956,81 @@ def head_backward(proto_nhwc: Tensor, pooled: Tensor, d_out: Optional[Tensor], w
               k, w_align, w_tanh, tanh_coeff, amax.data_ptr(), dpool.data_ptr(), d_logits.data_ptr(),
               _stream(proto_nhwc))
     return d_logits
+
+
+# ---- ResNet training: BatchNorm2d in train mode (csrc/bn_ops.hip) ----------------------------
+def _bn_ws(c: int, device) -> Tensor:
+    return torch.empty(int(_lib.load().pipnet_bn_workspace_floats(c)), device=device, dtype=torch.float32)
+
+
+def bn_stats(x: Tensor, eps: float, momentum: float, running_mean: Optional[Tensor] = None,
+             running_var: Optional[Tensor] = None) -> Tuple[Tensor, Tensor]:
+    """Batch mean / invstd over the rows of NHWC ``x`` (train-mode BatchNorm2d); updates the
+    running statistics in place when given (momentum, unbiased variance)."""
+    _chk(x, "BN input")
+    c = x.shape[-1]
+    m = x.numel() // c
+    mean = torch.empty(c, device=x.device, dtype=torch.float32)
+    invstd = torch.empty_like(mean)
+    for t, what in ((running_mean, "running_mean"), (running_var, "running_var")):
+        if t is not None:
+            _chk(t, what)
+    _lib.call("pipnet_bn_stats_f32", x.data_ptr(), m, c, eps, momentum, mean.data_ptr(), invstd.data_ptr(),
+              _ptr(running_mean), _ptr(running_var), _bn_ws(c, x.device).data_ptr(), _stream(x))
+    if running_mean is not None:
+        _mutated(running_mean, running_var)
+    return mean, invstd
+
+
+def bn_apply(x: Tensor, mean: Tensor, invstd: Tensor, gamma: Tensor, beta: Tensor, residual: Optional[Tensor] = None,
+             relu: bool = False, out: Optional[Tensor] = None) -> Tensor:
+    """gamma * (x - mean) * invstd + beta [+ residual] [ReLU] on NHWC rows."""
+    _chk(x, "BN input")
+    for t, what in ((gamma, "BN weight"), (beta, "BN bias")):
+        _chk(t, what)
+    if residual is not None:
+        _chk(residual, "residual")
+        if residual.shape != x.shape:
+            raise RuntimeError(f"bn_apply: residual {tuple(residual.shape)} vs {tuple(x.shape)}")
+    c = x.shape[-1]
+    y = torch.empty_like(x) if out is None else out
+    _lib.call("pipnet_bn_apply_f32", x.data_ptr(), x.numel() // c, c, mean.data_ptr(), invstd.data_ptr(),
+              gamma.data_ptr(), beta.data_ptr(), _ptr(residual), int(relu), y.data_ptr(), _stream(x))
+    return y
+
+
+def bn_backward(x: Tensor, dy: Tensor, mean: Tensor, invstd: Tensor, gamma: Tensor, relu_out: Optional[Tensor] = None,
+                want_dx: bool = True, want_masked: bool = False
+                ) -> Tuple[Optional[Tensor], Optional[Tensor], Tensor, Tensor]:
+    """Train-mode BatchNorm2d backward from the pre-norm rows ``x``; ``relu_out`` (the output of
+    the ReLU that follows, when there is one) masks dy.  Returns (dx, masked dy, d_gamma, d_beta)."""
+    _chk(x, "BN input")
+    _chk(dy, "BN output gradient")
+    if relu_out is not None:
+        _chk(relu_out, "ReLU output")
+    c = x.shape[-1]
+    dx = torch.empty_like(x) if want_dx else None
+    dm = torch.empty_like(x) if want_masked else None
+    dg = torch.empty(c, device=x.device, dtype=torch.float32)
+    db = torch.empty_like(dg)
+    _lib.call("pipnet_bn_backward_f32", x.data_ptr(), dy.data_ptr(), _ptr(relu_out), x.numel() // c, c, mean.data_ptr(),
+              invstd.data_ptr(), gamma.data_ptr(), _ptr(dx), _ptr(dm), dg.data_ptr(), db.data_ptr(),
+              _bn_ws(c, x.device).data_ptr(), _stream(x))
+    return dx, dm, dg, db
+
+
+def stride_scatter(x: Tensor, h: int, w: int, stride: int, out: Optional[Tensor] = None,
+                   accumulate: bool = False) -> Tensor:
+    """NHWC [B, OH, OW, C] -> [B, h, w, C] with x on the stride lattice, zeros elsewhere
+    (added into ``out`` when accumulate)."""
+    _chk(x, "scatter input")
+    b, oh, ow, c = x.shape
+    if out is None:
+        if accumulate:
+            raise RuntimeError("stride_scatter: accumulate needs out")
+        out = torch.empty((b, h, w, c), device=x.device, dtype=torch.float32)
+    elif tuple(out.shape) != (b, h, w, c):
+        raise RuntimeError(f"stride_scatter: out {tuple(out.shape)}")
+    _lib.call("pipnet_stride_scatter_f32", x.data_ptr(), b, oh, ow, c, h, w, stride, int(accumulate), out.data_ptr(),
+              _stream(x))
+    return out

@@ -1,5 +1,4 @@
-"""Finetune-phase PIP-Net training iteration on the MI355X kernels (SURVEY.md 8f rank 4,
-first slice).
+"""PIP-Net / CountPIPNet training iterations on the MI355X kernels.
 
 The reference trains with ``pipnet/train.py:train_pipnet`` (train.py:8-150).  In its
 finetune phase (main.py:333-345) only the classification layer trains, so one iteration is:
@@ -24,10 +23,11 @@ Stochastic-depth masks come from a host ``torch.Generator`` (the reference draws
 the device RNG: same distribution, different stream -- RNG parity unpinned; the tests
 inject the masks recorded from the reference).
 
-Other phases (pretrain, joint training) need backbone gradients: this package's modules
-run them on the torch autograd path under the reference's own ``train_pipnet`` (forward
-dispatches to torch whenever grad is enabled); HIP backward kernels for the trainable
-ConvNeXt stages are the next slice.
+The pretrain / joint / "train everything" phases backpropagate into a trainable backbone
+suffix on the same kernels: ConvNeXt CNBlocks / downsamples / stem (``_forward_saving``,
+``_block_backward``) and the ResNet-50 Bottlenecks with train-mode BatchNorm
+(``resnet_train``; every BN of the backbone, frozen ones included, normalises with batch
+statistics and updates its running statistics, as under the reference's ``net.train()``).
 """
 from __future__ import annotations
 
@@ -49,6 +49,37 @@ def _inner(net: nn.Module) -> nn.Module:
     return getattr(net, "module", net)
 
 
+def _is_resnet(m: nn.Module) -> bool:
+    from .resnet_features import ResNet_features
+    return isinstance(getattr(m, "_net", None), ResNet_features)
+
+
+def _backbone_ok(m: nn.Module) -> bool:
+    """A backbone with a HIP train-mode forward: ConvNeXt (full or mid-layer) or a Bottleneck
+    ResNet with the stem frozen (resnet_train.supported)."""
+    if isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+        return True
+    if _is_resnet(m):
+        from . import resnet_train
+        return resnet_train.supported(m._net)
+    return False
+
+
+def _sd_masks(m: nn.Module, batch: int, generator: Optional[torch.Generator]) -> Dict[int, Tensor]:
+    """Stochastic-depth keep masks of the backbone (ResNets have none)."""
+    if _is_resnet(m):
+        return {}
+    return stochastic_depth_masks(m._net.features, batch, generator)
+
+
+def _backbone_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor]) -> Tensor:
+    """Train-mode backbone forward without kept activations -> NHWC features."""
+    if _is_resnet(m):
+        from . import resnet_train
+        return resnet_train.train_forward(m._net, xs, None)[0]
+    return convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+
+
 def stochastic_depth_masks(features: nn.Sequential, batch: int,
                            generator: Optional[torch.Generator] = None) -> Dict[int, Tensor]:
     """Host keep masks (bool [batch]) for every CNBlock with p > 0, keyed by block id in
@@ -67,7 +98,7 @@ def hip_finetune_supported(net: nn.Module) -> bool:
     m = _inner(net)
     if hasattr(m, "_max_count") or not hasattr(m, "_classification"):
         return False
-    if not isinstance(m._net, (ConvNeXt, MidLayerConvNeXt)):
+    if not _backbone_ok(m):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
@@ -82,7 +113,7 @@ def train_forward_hip(net: nn.Module, xs: Tensor, sd_keep: Optional[Dict[int, Te
     from .pipnet import add_on_logits_hip
     m = _inner(net)
     with torch.no_grad():
-        feats = convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+        feats = _backbone_train_forward(m, xs, sd_keep)
         proto, pooled = K.softmax_pool(add_on_logits_hip(m._add_on, feats), pool_mode=0)
         _, out = K.nonneg_linear(pooled, m._classification.weight, m._classification.bias, None)
     return proto, pooled, out
@@ -129,7 +160,7 @@ def hip_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor,
     cls = m._classification
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
-        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+        sd_keep = _sd_masks(m, xs.shape[0], generator)
     proto, pooled, out = train_forward_hip(m, xs, sd_keep)
     w_align, w_tanh, w_class = FINETUNE_LOSS_WEIGHTS
     with torch.no_grad():
@@ -165,7 +196,7 @@ def hip_count_finetune_supported(net: nn.Module) -> bool:
     from .count_pipnet_utils import (BilinearIntermediate, IdentityIntermediate, LinearFull, LinearIntermediate,
                                      OneHotEncoder)
     m = _inner(net)
-    if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+    if not hasattr(m, "_max_count") or not _backbone_ok(m):
         return False
     if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, LinearIntermediate,
                                        BilinearIntermediate)):
@@ -187,9 +218,9 @@ def _count_train_forward(m: nn.Module, xs: Tensor, sd_keep: Dict[int, Tensor], j
     from .pipnet import add_on_logits_hip
     saved = {}
     if j is None:
-        feats = convnext_features_hip(m._net.features, xs, m._net._hip_pack, sd_keep)
+        feats = _backbone_train_forward(m, xs, sd_keep)
     else:
-        feats, saved["suffix"] = _forward_saving(m, xs, j, sd_keep)
+        feats, saved["suffix"] = _backbone_forward_saving(m, xs, j, sd_keep)
         saved["feats"] = feats
     act = list(m._add_on)[-1] if isinstance(m._add_on, nn.Sequential) else m._add_on
     if isinstance(act, GumbelSoftmax):
@@ -285,7 +316,7 @@ def hip_count_finetune_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor
     cls = m._classification
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
-        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+        sd_keep = _sd_masks(m, xs.shape[0], generator)
     w_align, w_tanh, w_class = FINETUNE_LOSS_WEIGHTS
     with torch.no_grad():
         proto, counts, clamped, saved, inter, out = _count_train_forward(m, xs, sd_keep)
@@ -328,12 +359,33 @@ def _cnblocks(seq) -> list:
 
 
 def trainable_suffix_start(net: nn.Module) -> int:
-    """Index j of the first ``features`` entry holding a trainable parameter (len(features)
-    when the backbone is frozen).  Gradients flow through every entry of features[j:]."""
-    for j, mod in enumerate(_inner(net)._net.features):
+    """Index j of the first ``features`` entry (ConvNeXt) or residual block (ResNet) holding a
+    trainable parameter (their count when the backbone is frozen).  Gradients flow through
+    every entry from j on."""
+    m = _inner(net)
+    if _is_resnet(m):
+        from . import resnet_train
+        return resnet_train.trainable_start(m._net)
+    for j, mod in enumerate(m._net.features):
         if any(p.requires_grad for p in mod.parameters()):
             return j
-    return len(_inner(net)._net.features)
+    return len(m._net.features)
+
+
+def _backbone_units(m: nn.Module) -> int:
+    if _is_resnet(m):
+        from . import resnet_train
+        return len(resnet_train._blocks(m._net))
+    return len(m._net.features)
+
+
+def _backbone_forward_saving(m: nn.Module, xs: Tensor, j: int, sd_keep: Dict[int, Tensor]):
+    """Train-mode backbone forward keeping the activations of the trainable suffix from j."""
+    if _is_resnet(m):
+        from . import resnet_train
+        feats, saved = resnet_train.train_forward(m._net, xs, j)
+        return feats, [("resnet", None, None, saved)]
+    return _forward_saving(m, xs, j, sd_keep)
 
 
 def hip_train_supported(net: nn.Module) -> bool:
@@ -341,11 +393,11 @@ def hip_train_supported(net: nn.Module) -> bool:
     (the reference's pretrain / "train + freeze params" phases; j = 0, the stem included: the
     "train everything" epochs after freeze_epochs, main.py:362-373)."""
     m = _inner(net)
-    if hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+    if hasattr(m, "_max_count") or not _backbone_ok(m):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
-    return trainable_suffix_start(m) < len(m._net.features)
+    return trainable_suffix_start(m) < _backbone_units(m)
 
 
 def _forward_saving(m: nn.Module, xs: Tensor, j: int, sd_keep: Dict[int, Tensor]):
@@ -514,6 +566,11 @@ def _addon_suffix_backward(m: nn.Module, feats: Tensor, saved: list, d_logits: T
         dy = dy.view(bsz, hh, ww, cf)
     else:
         dy = d_logits
+    if saved and saved[0][0] == "resnet":
+        from . import resnet_train
+        resnet_train.backward(m._net, saved[0][3], dy)
+        saved.clear()
+        return
     for i in range(len(saved) - 1, -1, -1):
         kind, mod, _, sv = saved[i]
         if kind == "block":
@@ -563,15 +620,15 @@ def hip_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimiz
     from .pipnet import add_on_logits_hip
     m = _inner(net)
     j = trainable_suffix_start(m)
-    if j >= len(m._net.features):
+    if j >= _backbone_units(m):
         raise NotImplementedError("HIP training step: no trainable backbone parameter (use the finetune step)")
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
-        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+        sd_keep = _sd_masks(m, xs.shape[0], generator)
     cls = m._classification
     w_align, w_tanh, w_class = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
     with torch.no_grad():
-        feats, saved = _forward_saving(m, xs, j, sd_keep)
+        feats, saved = _backbone_forward_saving(m, xs, j, sd_keep)
         logits = add_on_logits_hip(m._add_on, feats)
         proto, pooled = K.softmax_pool(logits, pool_mode=0)
         _, out = K.nonneg_linear(pooled, cls.weight, cls.bias, None)
@@ -597,14 +654,14 @@ def hip_count_train_supported(net: nn.Module) -> bool:
     from .count_pipnet_utils import (BilinearIntermediate, IdentityIntermediate, LinearFull, LinearIntermediate,
                                      OneHotEncoder)
     m = _inner(net)
-    if not hasattr(m, "_max_count") or not isinstance(getattr(m, "_net", None), (ConvNeXt, MidLayerConvNeXt)):
+    if not hasattr(m, "_max_count") or not _backbone_ok(m):
         return False
     if not isinstance(m._intermediate, (IdentityIntermediate, OneHotEncoder, LinearFull, LinearIntermediate,
                                        BilinearIntermediate)):
         return False
     if not all(p.is_cuda and p.dtype == torch.float32 for p in m.parameters()):
         return False
-    return trainable_suffix_start(m) < len(m._net.features)
+    return trainable_suffix_start(m) < _backbone_units(m)
 
 
 def hip_count_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, optimizer_net, optimizer_classifier,
@@ -621,11 +678,11 @@ def hip_count_train_step(net: nn.Module, xs1: Tensor, xs2: Tensor, ys: Tensor, o
     and the sparsity clamps as ``hip_train_step``.  Returns the loss-kernel stats."""
     m = _inner(net)
     j = trainable_suffix_start(m)
-    if j >= len(m._net.features):
+    if j >= _backbone_units(m):
         raise NotImplementedError("HIP count training step: no trainable backbone parameter (use the finetune step)")
     xs = torch.cat([xs1, xs2])
     if sd_keep is None:
-        sd_keep = stochastic_depth_masks(m._net.features, xs.shape[0], generator)
+        sd_keep = _sd_masks(m, xs.shape[0], generator)
     cls = m._classification
     w_align, w_tanh, w_class = (epoch / nr_epochs, 5.0, 0.0) if pretrain else FINETUNE_LOSS_WEIGHTS
     with torch.no_grad():
@@ -712,10 +769,12 @@ def train_pipnet(net, train_loader, optimizer_net, optimizer_classifier, schedul
                  progress_prefix: str = "Train Epoch", enforce_weight_sparsity=True, tanh_loss_coeff=1.0,
                  generator: Optional[torch.Generator] = None, verbose: bool = False) -> dict:
     """Drop-in for train.py:8-150 (same arguments, same ``train_info`` keys; progress output
-    reduced to one optional line) for a ConvNeXt PIP-Net: the finetune phase
-    (``hip_finetune_step``) and the pretrain / joint phases with a trainable backbone suffix
-    (``hip_train_step``).  Anything else (CountPIPNet, ResNet, a trainable stem) raises --
-    run the reference's own loop on these modules (torch autograd path)."""
+    reduced to one optional line) for a ConvNeXt or ResNet-50 PIP-Net and a ConvNeXt
+    CountPIPNet: the finetune phase (``hip_finetune_step`` / ``hip_count_finetune_step``) and
+    the pretrain / joint / "train everything" phases with a trainable backbone suffix
+    (``hip_train_step`` / ``hip_count_train_step``).  Anything else (a trainable ResNet stem,
+    an intermediate layer without a HIP backward, non-fp32 parameters) raises -- run the
+    reference's own loop on these modules (torch autograd path)."""
     if pretrain and finetune:
         raise NotImplementedError("count_pipnet_amd.train_pipnet: pretrain and finetune are exclusive")
     if is_count_pipnet and finetune:

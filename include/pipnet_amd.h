@@ -354,12 +354,13 @@ int pipnet_wgrad_f32(const float* A, int64_t lda, const float* B, int64_t ldb, i
  *   [B,H,W,Cin]; workspace: pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, 4*Cin) bytes. */
 int pipnet_wgrad_conv2x2_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int stride, int Cout,
                              float* dW, int accumulate, float* workspace, void* stream);
-/* pipnet_wgrad_conv_f32: weight gradient of a KHxKW conv, stride s, no padding (the ConvNeXt
- * stem, torchvision Conv2dNormActivation(3, 96, 4, 4) with Cin zero-padded to 4): dY NHWC
- * [B][OH][OW][Cout], x NHWC [B][H][W][Cin] -> dW [Cout][KH][KW][Cin] (accumulate adds);
- * workspace: pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, KH*KW*Cin). */
+/* pipnet_wgrad_conv_f32: weight gradient of a KHxKW conv, stride s, zero padding p (the
+ * ConvNeXt stem, Conv2d(3, 96, 4, 4) with Cin zero-padded to 4; the ResNet 3x3 / strided 1x1
+ * convs, features/resnet_features.py:17-28): dY NHWC [B][OH][OW][Cout], x NHWC [B][H][W][Cin]
+ * -> dW [Cout][KH][KW][Cin] (accumulate adds); OH = (H + 2p - KH) / s + 1; workspace:
+ * pipnet_wgrad_workspace_bytes(B*OH*OW, Cout, KH*KW*Cin). */
 int pipnet_wgrad_conv_f32(const float* dY, const float* x, int B, int H, int W, int Cin, int KH, int KW, int stride,
-                          int Cout, float* dW, int accumulate, float* workspace, void* stream);
+                          int pad, int Cout, float* dW, int accumulate, float* workspace, void* stream);
 int pipnet_colsum_workspace_bytes(int N);
 int pipnet_colsum_f32(const float* A, int64_t lda, int M, int N, float* out, int accumulate, float* workspace,
                       void* stream);
@@ -419,6 +420,32 @@ int pipnet_onehot_ste_bwd_f32(const float* x, int64_t rows, int M, const float* 
 int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, int HW, int P, const float* d_counts_in,
                               float w_align, float w_tanh, float tanh_coeff, float inv_tau, float* dcnt_ws,
                               float* d_logits, void* stream);
+
+/* ---- ResNet training step (csrc/bn_ops.hip): BatchNorm2d in train mode ------------------
+ * Replaces the autograd of nn.BatchNorm2d(C) under net.train() in the ResNet Bottleneck /
+ * stem (features/resnet_features.py:77-119, 137-140; pipnet/train.py:14), NHWC rows
+ * x[M][C], M = B*H*W, C % 4 == 0 (and C/4 >= 64 or dividing 256), 16-B aligned operands.
+ * pipnet_bn_stats_f32: mean / invstd of the batch (two-pass biased variance, eps), and when
+ *   running_mean / running_var are given the momentum update with the unbiased variance
+ *   (torch semantics); M >= 2 (torch: "Expected more than 1 value per channel").
+ * pipnet_bn_apply_f32: y = gamma (x - mean) invstd + beta [+ residual] [ReLU].
+ * pipnet_bn_backward_f32: g = dy [* (relu_out > 0)]; d_beta = sum g, d_gamma = sum g xhat,
+ *   dx = gamma invstd (g - d_beta/M - xhat d_gamma/M) (dx NULL: parameters only); d_masked
+ *   (optional) receives g -- the identity-path gradient of a residual block.
+ *   workspace: pipnet_bn_workspace_floats(C) floats, for both calls.
+ * pipnet_stride_scatter_f32: out[B][H][W][C] (+)= in[B][OH][OW][C] placed on the stride
+ *   lattice (zeros elsewhere): the input gradient of a stride-s 1x1 conv, and the
+ *   zero-inserted gradient a stride-s 3x3 conv's input gradient is convolved from. */
+int64_t pipnet_bn_workspace_floats(int C);
+int pipnet_bn_stats_f32(const float* x, int64_t M, int C, float eps, float momentum, float* mean, float* invstd,
+                        float* running_mean, float* running_var, float* workspace, void* stream);
+int pipnet_bn_apply_f32(const float* x, int64_t M, int C, const float* mean, const float* invstd, const float* gamma,
+                        const float* beta, const float* residual, int relu, float* y, void* stream);
+int pipnet_bn_backward_f32(const float* x, const float* dy, const float* relu_out, int64_t M, int C,
+                           const float* mean, const float* invstd, const float* gamma, float* dx, float* d_masked,
+                           float* d_gamma, float* d_beta, float* workspace, void* stream);
+int pipnet_stride_scatter_f32(const float* in, int B, int OH, int OW, int C, int H, int W, int stride, int accumulate,
+                              float* out, void* stream);
 
 #ifdef __cplusplus
 }

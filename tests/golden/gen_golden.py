@@ -75,6 +75,10 @@ CASES = {
     # C3: PIP-Net ResNet50, 224x224
     "c3_pipnet_resnet50": dict(model="pipnet", net="resnet50", num_features=0, bias=False,
                                num_classes=200, batch=2, size=224, seed=31),
+    # ResNet-50 PIP-Net at 64x64 (8x8 feature map): the forward case of the ResNet training
+    # fixtures (gen_golden_train.py)
+    "pipnet_resnet50_small": dict(model="pipnet", net="resnet50", num_features=0, bias=False,
+                                  num_classes=10, batch=2, size=64, seed=32),
 }
 PROFILE = "trained"
 

@@ -74,6 +74,13 @@ TRAIN_CASES = {
     "train_full_mid_addon": ("pipnet_mid_addon", 2, 3, 313, True, "full"),
     "train_full_c2": ("c2_pipnet_convnext26", 2, 2, 314, False, "full"),
     "train_count_full_onehot": ("count_onehot", 2, 3, 315, True, "count_full"),
+    # ResNet-50 (util/args.py:280-290 groups; every BatchNorm2d in train mode, running
+    # statistics recorded): finetune, pretrain, "train + freeze params" (layer3 / layer4) and
+    # "train everything" (layer2 too; the stem and layer1 never train)
+    "train_finetune_resnet50": ("pipnet_resnet50_small", 2, 2, 320, False, "finetune"),
+    "train_pretrain_resnet50": ("pipnet_resnet50_small", 2, 2, 321, False, "pretrain"),
+    "train_joint_resnet50": ("pipnet_resnet50_small", 2, 2, 322, False, "joint"),
+    "train_full_resnet50": ("pipnet_resnet50_small", 2, 2, 323, False, "full"),
 }
 LR, WD = 0.05, 0.01
 
@@ -175,7 +182,8 @@ def run(name):
             rec[key + "_rowsum"] = a.astype(np.float64).sum(axis=1)
     for i, ((xs1, xs2, ys), s) in enumerate(zip(batches, seen)):
         rec[f"s{i}_ys"] = ys.numpy()
-        rec[f"s{i}_masks"] = torch.stack(drawn[i * nmask:(i + 1) * nmask]).numpy()
+        rec[f"s{i}_masks"] = (torch.stack(drawn[i * nmask:(i + 1) * nmask]).numpy() if nmask
+                              else np.zeros((0, 2 * bs), dtype=np.float32))
         for k in ("pooled", "out", "b", "mult", "proto"):
             if s[k] is not None:
                 rec[f"s{i}_{k}"] = s[k].numpy()
@@ -194,6 +202,14 @@ def run(name):
                 st_p = opt_net.state.get(prm, {})
                 if "exp_avg_sq" in st_p:
                     rec[f"param/{pname}/v_head"] = st_p["exp_avg_sq"].flatten()[:256].numpy()
+    for bname, buf in net.named_buffers():          # BatchNorm running statistics (ResNet)
+        if bname.endswith(("running_mean", "running_var")):
+            a = buf.detach().double()
+            rec[f"buffer/{bname}/sum"] = np.array(float(a.sum()))
+            rec[f"buffer/{bname}/abs"] = np.array(float(a.abs().sum()))
+            rec[f"buffer/{bname}/head"] = buf.detach().flatten()[:64].numpy()
+        elif bname.endswith("num_batches_tracked"):
+            rec[f"buffer/{bname}"] = buf.detach().numpy()
     cls = net._classification
     put("final_w", cls.weight)
     rec["final_mult"] = cls.normalization_multiplier.detach().numpy()

@@ -160,18 +160,22 @@ def _finetune_setup(name, gpu):
 
 def _sd_keep(net, masks):
     """Recorded masks (forward order of the blocks with p > 0) -> {block id: bool mask}."""
+    if not hasattr(net._net, "features"):         # ResNet: no stochastic depth
+        assert masks.shape[0] == 0
+        return {}
     blocks = [m for m in net._net.features.modules() if isinstance(m, CNBlock)]
     ids = [bid for bid, b in enumerate(blocks) if b.stochastic_depth.p > 0.0]
     assert len(ids) == masks.shape[0]
     return {bid: _t(masks[j]) > 0.5 for j, bid in enumerate(ids)}
 
 
-def _quorum_close(a, b, rtol, atol, frac=0.99, max_abs=None):
+def _quorum_close(a, b, rtol, atol, frac=0.99, max_abs=None, what=""):
     a, b = a.detach().cpu().double(), b.detach().cpu().double()
     ok = (a - b).abs() <= atol + rtol * b.abs()
-    assert ok.float().mean().item() >= frac, f"{(~ok).sum().item()} / {ok.numel()} elements differ"
+    assert ok.float().mean().item() >= frac, \
+        f"{what}: {(~ok).sum().item()} / {ok.numel()} elements differ (max |diff| {(a - b).abs().max().item():.3g})"
     if max_abs is not None:
-        assert (a - b).abs().max().item() <= max_abs
+        assert (a - b).abs().max().item() <= max_abs, what
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -252,7 +256,14 @@ def _optimizers_like_reference(net, meta, fwd_meta):
     train, freeze, backbone = [], [], []
     for name, prm in net._net.named_parameters():
         parts = name.split(".")
-        if case.get("use_mid_layers"):
+        if case["net"].startswith("resnet"):     # util/args.py:280-290
+            if "layer4.2" in name:
+                train.append(prm)
+            elif "layer4" in name or "layer3" in name:
+                freeze.append(prm)
+            elif "layer2" in name:
+                backbone.append(prm)
+        elif case.get("use_mid_layers"):
             st = int(parts[1])
             (train if st == case["num_stages"] else freeze if st == case["num_stages"] - 1 else backbone).append(prm)
         else:
@@ -312,21 +323,63 @@ def test_suffix_training_matches_reference(gpu, name):
     assert names
     params = dict(net.named_parameters())
     lr_max = max(g["lr"] for g in opt_net.param_groups) * 1.0
+    resnet = fwd_meta["case"]["net"].startswith("resnet")
     for pname in names:
         p = params[pname].detach().cpu().double()
         head = _t(rec[f"param/{pname}/head"]).double()
+        if resnet:
+            # fp32 ResNet-50 backprop is ~2 % from fp64 for torch as well (see
+            # _resnet_grads_vs_f64), so AdamW's sign-like first steps may differ: every element
+            # within the AdamW step bound (2 lr per iteration), no quorum
+            lr_p = next(g["lr"] for g in opt_net.param_groups if any(q is params[pname] for q in g["params"]))
+            bound = 2.0 * meta["iterations"] * max(lr_p, meta["lr_net"], meta["lr_block"]) * 1.001 + 1e-7
+            assert (p.flatten()[:head.numel()] - head).abs().max().item() <= bound, pname
+            continue
         _quorum_close(p.flatten()[:head.numel()], head, 1e-4, 1e-6, frac=0.95,
-                      max_abs=2.5 * meta["iterations"] * 10 * meta["lr_block"] + 1e-6)
+                      max_abs=2.5 * meta["iterations"] * 10 * meta["lr_block"] + 1e-6, what=pname)
         ref_abs = float(rec[f"param/{pname}/abs"])
         assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
+    _check_running_stats(net, rec)
     cls = net._classification
-    if not pretrain:
+    if not pretrain and resnet:
+        # iteration 2's classifier gradient sees the backbone after one AdamW step whose
+        # sign-like updates differ where fp32 backprop does (see above): AdamW step bound
+        w8 = _t(rec["final_w_rows8"]).double()
+        assert (cls.weight[:8].detach().cpu().double() - w8).abs().max().item() <= 2 * meta["lr"] * iters * 1.001
+    elif not pretrain:
         if "final_w" in rec:
             _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, frac=0.97,
                           max_abs=4 * meta["lr"] * iters + 1e-6)
         else:
             _quorum_close(cls.weight[:8], _t(rec["final_w_rows8"]), 1e-4, 1e-5, frac=0.97,
                           max_abs=4 * meta["lr"] * iters + 1e-6)
+
+
+def _check_running_stats(net, rec):
+    """BatchNorm running statistics after the run == the reference's (every BN of the backbone
+    runs in train mode, frozen layers included): sums and the first 64 values of every BN in
+    the frozen prefix (stem and the blocks before the first trainable one -- the later ones
+    see weights the two runs' AdamW steps moved by sign-like amounts), and every counter."""
+    from count_pipnet_amd import resnet_train as R
+    if not hasattr(net._net, "layer1"):
+        return
+    start = R.trainable_start(net._net)
+    prefix = ["_net.bn1."] + [f"_net.{k}." for k, _ in R._blocks(net._net)[:start]]
+    bufs = dict(net.named_buffers())
+    names = [k[len("buffer/"):-len("/sum")] for k in rec if k.startswith("buffer/") and k.endswith("/sum")]
+    checked = 0
+    for bname in names:
+        if not bname.startswith(tuple(prefix)):
+            continue
+        b = bufs[bname].detach().cpu().double()
+        head = _t(rec[f"buffer/{bname}/head"]).double()
+        torch.testing.assert_close(b.flatten()[:head.numel()], head, rtol=1e-3, atol=1e-5, msg=bname)
+        assert float(b.abs().sum()) == pytest.approx(float(rec[f"buffer/{bname}/abs"]), rel=1e-3, abs=1e-5)
+        checked += 1
+    assert checked >= 2
+    for k in rec:
+        if k.startswith("buffer/") and k.endswith("num_batches_tracked"):
+            assert int(bufs[k[len("buffer/"):]]) == int(rec[k]), k
 
 
 def _torch_path_grads(net, xs, ys, masks_in_order, w_align, w_tanh, w_class, mult):
@@ -375,11 +428,40 @@ def test_suffix_gradients_match_autograd(gpu, name):
     ref = _torch_path_grads(net, torch.cat([xs1, xs2]).to(gpu), ys.to(gpu), masks, wa, wt, wc,
                             float(net._classification.normalization_multiplier[0]))
     assert set(hip) == set(ref), (sorted(set(hip) ^ set(ref)))
+    if fwd_meta["case"]["net"].startswith("resnet"):
+        _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref, (wa, wt, wc), gpu)
+        return
     for n in sorted(ref):
         a, b = hip[n].double(), ref[n].double()
         scale = b.abs().max().item() + 1e-12
         err = (a - b).abs().max().item() / scale
         assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"
+
+
+def _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref32, weights, gpu):
+    """ResNet-50 backprop through 13-16 train-mode BatchNorm blocks is ill-conditioned in fp32:
+    torch's own fp32 autograd lands ~2 % (median over parameters, max-normalised) from fp64
+    autograd on these fixtures, whatever the batch or image size (scratch measurements in
+    DESIGN.md section 4).  Yardstick: the HIP gradients must be as close to fp64 autograd as
+    torch fp32 is -- median error within 2x torch's, worst parameter within 3x torch's worst
+    -- and every parameter within 25 % (a wrong stride / padding / mask is O(1))."""
+    import copy
+    import statistics
+    net64 = copy.deepcopy(net).double()
+    for p in net64.parameters():
+        p.grad = None
+    ref64 = _torch_path_grads(net64, torch.cat([xs1, xs2]).to(gpu).double(), ys.to(gpu), [], *weights,
+                              float(net._classification.normalization_multiplier[0]))
+    eh, et = {}, {}
+    for n in ref64:
+        b = ref64[n].double()
+        s = b.abs().max().item() + 1e-30
+        eh[n] = (hip[n].double() - b).abs().max().item() / s
+        et[n] = (ref32[n].double() - b).abs().max().item() / s
+    worst = max(eh, key=eh.get)
+    assert statistics.median(eh.values()) <= 2 * statistics.median(et.values()) + 1e-4, (eh, et)
+    assert eh[worst] <= 3 * max(et.values()) + 1e-4, (worst, eh[worst], max(et.values()))
+    assert eh[worst] < 0.25, (worst, eh[worst])
 
 
 # ---- CountPIPNet finetune phase: classifier + intermediate layer (main.py:333-343) -----------
@@ -550,11 +632,40 @@ def test_count_suffix_gradients_match_autograd(gpu, name):
     ref = _torch_path_grads(net, torch.cat([xs1, xs2]).to(gpu), ys.to(gpu), masks, wa, wt, wc,
                             float(net._classification.normalization_multiplier[0]))
     assert set(hip) == set(ref), (sorted(set(hip) ^ set(ref)))
+    if fwd_meta["case"]["net"].startswith("resnet"):
+        _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref, (wa, wt, wc), gpu)
+        return
     for n in sorted(ref):
         a, b = hip[n].double(), ref[n].double()
         scale = b.abs().max().item() + 1e-12
         err = (a - b).abs().max().item() / scale
         assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"
+
+
+def _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref32, weights, gpu):
+    """ResNet-50 backprop through 13-16 train-mode BatchNorm blocks is ill-conditioned in fp32:
+    torch's own fp32 autograd lands ~2 % (median over parameters, max-normalised) from fp64
+    autograd on these fixtures, whatever the batch or image size (scratch measurements in
+    DESIGN.md section 4).  Yardstick: the HIP gradients must be as close to fp64 autograd as
+    torch fp32 is -- median error within 2x torch's, worst parameter within 3x torch's worst
+    -- and every parameter within 25 % (a wrong stride / padding / mask is O(1))."""
+    import copy
+    import statistics
+    net64 = copy.deepcopy(net).double()
+    for p in net64.parameters():
+        p.grad = None
+    ref64 = _torch_path_grads(net64, torch.cat([xs1, xs2]).to(gpu).double(), ys.to(gpu), [], *weights,
+                              float(net._classification.normalization_multiplier[0]))
+    eh, et = {}, {}
+    for n in ref64:
+        b = ref64[n].double()
+        s = b.abs().max().item() + 1e-30
+        eh[n] = (hip[n].double() - b).abs().max().item() / s
+        et[n] = (ref32[n].double() - b).abs().max().item() / s
+    worst = max(eh, key=eh.get)
+    assert statistics.median(eh.values()) <= 2 * statistics.median(et.values()) + 1e-4, (eh, et)
+    assert eh[worst] <= 3 * max(et.values()) + 1e-4, (worst, eh[worst], max(et.values()))
+    assert eh[worst] < 0.25, (worst, eh[worst])
 
 
 def test_count_train_pipnet_joint_epoch(gpu):
@@ -567,6 +678,35 @@ def test_count_train_pipnet_joint_epoch(gpu):
                               is_count_pipnet=True)
     assert len(info["lrs_class"]) == len(batches) and len(info["lrs_net"]) == len(batches)
     assert np.isfinite(info["loss"]) and info["loss"] > 0
+
+
+@pytest.mark.parametrize("phase", ["joint", "finetune"])
+def test_train_pipnet_resnet_epoch(gpu, phase):
+    """count_pipnet_amd.train_pipnet drives the HIP ResNet-50 steps (train-mode BatchNorm,
+    backward through layer3 / layer4) and reproduces the reference epoch's loss terms."""
+    meta, rec, fwd_meta = load_train_golden(f"train_{phase}_resnet50")
+    net = build_model(fwd_meta).to(gpu).train()
+    if phase == "finetune":
+        meta2 = dict(meta, phase="finetune")
+        opt_net, opt_cls, sched_net, sched_cls = _optimizers_like_reference(net, meta2, fwd_meta)
+        for prm in net.parameters():
+            prm.requires_grad = False
+        for prm in net._classification.parameters():
+            prm.requires_grad = True
+        net._classification.normalization_multiplier.requires_grad = False
+    else:
+        opt_net, opt_cls, sched_net, sched_cls = _optimizers_like_reference(net, meta, fwd_meta)
+    c = fwd_meta["case"]
+    batches = train_loader_batches(c["size"], c["num_classes"], meta["iterations"], meta["batch_per_view"],
+                                   meta["seed"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        info = T.train_pipnet(net, batches, opt_net, opt_cls, sched_net, sched_cls, None, 1, 1, gpu,
+                              finetune=phase == "finetune")
+    ref = meta["info"]
+    for k in ("align_loss_raw", "tanh_loss_raw", "class_loss_raw", "loss"):
+        assert info[k] == pytest.approx(ref[k], rel=2e-3, abs=1e-4), k
+    assert info["train_accuracy"] == pytest.approx(ref["train_accuracy"])
+    assert info["lrs_class"] == pytest.approx(ref["lrs_class"])
 
 
 @pytest.mark.parametrize("b,p,e,want_dx", [(1, 1, 1, True), (4, 16, 3, True), (7, 2048, 3, False),
