@@ -200,15 +200,15 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
         for (int e = 0; e < 4; ++e) xv[e] = xv[e] < thresh ? 0.f : xv[e];
       }
       if (x_out && blockIdx.y == 0) st4(x_out + (int64_t)b * D + c, xv);
+      // rows past nk load row nk-1 and are discarded: a load under a per-class branch
+      // made the compiler wait for each one (16 serialised round trips per slice)
 #pragma unroll
       for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
-        if (j < nk) {
-          const f32x4 w = ld4(w0 + (int64_t)j * D + c);
-          s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
-          s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
-          s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
-          s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
-        }
+        const f32x4 w = ld4(w0 + (int64_t)(j < nk ? j : nk - 1) * D + c);
+        s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
+        s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
+        s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
+        s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
       }
     }
   } else {
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
       if (x_out && blockIdx.y == 0) x_out[(int64_t)b * D + c] = xv;
 #pragma unroll
       for (int j = 0; j < NN_CLS_PER_BLOCK; ++j)
-        if (j < nk) s[j] = fmaf(xv, fmaxf(w0[(int64_t)j * D + c], 0.f), s[j]);
+        s[j] = fmaf(xv, fmaxf(w0[(int64_t)(j < nk ? j : nk - 1) * D + c], 0.f), s[j]);
     }
   }
 #pragma unroll

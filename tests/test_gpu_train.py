@@ -441,9 +441,9 @@ def test_suffix_gradients_match_autograd(gpu, name):
 def _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref32, weights, gpu):
     """ResNet-50 backprop through 13-16 train-mode BatchNorm blocks is ill-conditioned in fp32:
     torch's own fp32 autograd lands ~2 % (median over parameters, max-normalised) from fp64
-    autograd on these fixtures, whatever the batch or image size (scratch measurements in
-    DESIGN.md section 4).  Yardstick: the HIP gradients must be as close to fp64 autograd as
-    torch fp32 is -- median error within 2x torch's, worst parameter within 3x torch's worst
+    autograd on these fixtures, whatever the batch or image size
+    (tools/resnet_grad_conditioning.py, profiles/r02/resnet_grad_conditioning.txt).  Yardstick:
+    the HIP gradients must be as close to fp64 autograd as torch fp32 is -- median error within 2x torch's, worst parameter within 3x torch's worst
     -- and every parameter within 25 % (a wrong stride / padding / mask is O(1))."""
     import copy
     import statistics
@@ -632,40 +632,11 @@ def test_count_suffix_gradients_match_autograd(gpu, name):
     ref = _torch_path_grads(net, torch.cat([xs1, xs2]).to(gpu), ys.to(gpu), masks, wa, wt, wc,
                             float(net._classification.normalization_multiplier[0]))
     assert set(hip) == set(ref), (sorted(set(hip) ^ set(ref)))
-    if fwd_meta["case"]["net"].startswith("resnet"):
-        _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref, (wa, wt, wc), gpu)
-        return
     for n in sorted(ref):
         a, b = hip[n].double(), ref[n].double()
         scale = b.abs().max().item() + 1e-12
         err = (a - b).abs().max().item() / scale
         assert err < 2e-3, f"{n}: max |hip - autograd| / max|autograd| = {err:.3g}"
-
-
-def _resnet_grads_vs_f64(net, xs1, xs2, ys, hip, ref32, weights, gpu):
-    """ResNet-50 backprop through 13-16 train-mode BatchNorm blocks is ill-conditioned in fp32:
-    torch's own fp32 autograd lands ~2 % (median over parameters, max-normalised) from fp64
-    autograd on these fixtures, whatever the batch or image size (scratch measurements in
-    DESIGN.md section 4).  Yardstick: the HIP gradients must be as close to fp64 autograd as
-    torch fp32 is -- median error within 2x torch's, worst parameter within 3x torch's worst
-    -- and every parameter within 25 % (a wrong stride / padding / mask is O(1))."""
-    import copy
-    import statistics
-    net64 = copy.deepcopy(net).double()
-    for p in net64.parameters():
-        p.grad = None
-    ref64 = _torch_path_grads(net64, torch.cat([xs1, xs2]).to(gpu).double(), ys.to(gpu), [], *weights,
-                              float(net._classification.normalization_multiplier[0]))
-    eh, et = {}, {}
-    for n in ref64:
-        b = ref64[n].double()
-        s = b.abs().max().item() + 1e-30
-        eh[n] = (hip[n].double() - b).abs().max().item() / s
-        et[n] = (ref32[n].double() - b).abs().max().item() / s
-    worst = max(eh, key=eh.get)
-    assert statistics.median(eh.values()) <= 2 * statistics.median(et.values()) + 1e-4, (eh, et)
-    assert eh[worst] <= 3 * max(et.values()) + 1e-4, (worst, eh[worst], max(et.values()))
-    assert eh[worst] < 0.25, (worst, eh[worst])
 
 
 def test_count_train_pipnet_joint_epoch(gpu):
