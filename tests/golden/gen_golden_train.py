@@ -156,6 +156,26 @@ def run(name):
         return loss, acc, comp
 
     ref_train.calculate_loss = rec_loss
+    # every iteration's gradients as the optimizers see them (first 256 values per tensor;
+    # 2048 of the classifier weight): the tests derive per-element AdamW step tolerances
+    # from them (an element whose gradient is decisive in every step must follow the
+    # reference's trajectory closely, one whose gradient is near zero may flip its sign-like
+    # step)
+    grads = {"net": [], "cls": []}
+
+    def recording(opt, key, limit):
+        orig = opt.step
+
+        def step(*a, **kw):
+            mine = {id(q) for g in opt.param_groups for q in g["params"]}
+            grads[key].append({n: p.grad.detach().flatten()[:limit].clone() for n, p in net.named_parameters()
+                               if p.grad is not None and p.requires_grad and id(p) in mine})
+            return orig(*a, **kw)
+        opt.step = step
+        return orig
+
+    orig_net_step = recording(opt_net, "net", 256)
+    orig_cls_step = recording(opt_cls, "cls", 2048)
     h = net.register_forward_hook(hook)
     try:
         with injected_bernoulli(seed=5000 + seed) as drawn, G.injected_exponential(seed=7000 + seed) as noise, \
@@ -169,6 +189,7 @@ def run(name):
     finally:
         h.remove()
         ref_train.calculate_loss = orig_loss
+        opt_net.step, opt_cls.step = orig_net_step, orig_cls_step
     nmask = len(drawn) // nb
     rec = {}
 
@@ -202,6 +223,10 @@ def run(name):
                 st_p = opt_net.state.get(prm, {})
                 if "exp_avg_sq" in st_p:
                     rec[f"param/{pname}/v_head"] = st_p["exp_avg_sq"].flatten()[:256].numpy()
+    for key in ("net", "cls"):
+        for i, gd in enumerate(grads[key]):
+            for pname, g in gd.items():
+                rec[f"grad{i}/{pname}"] = g.numpy()
     for bname, buf in net.named_buffers():          # BatchNorm running statistics (ResNet)
         if bname.endswith(("running_mean", "running_var")):
             a = buf.detach().double()

@@ -7,7 +7,8 @@
 * end to end: count_pipnet_amd.train on the HIP model with the reference's weights, images,
   labels and recorded stochastic-depth masks reproduces the reference's loss terms and its
   classifier / AdamW state after every iteration (fp32 forward parity ~1e-5 feeds Adam's
-  sign-like first steps, so weights are compared elementwise with a 99 % quorum);
+  sign-like first steps, so every weight is held to a per-element AdamW step tolerance
+  derived from the reference's recorded gradients -- no quorum);
 * the HIP forward in train mode (stochastic depth) == the oracle forward with the same masks.
 """
 import contextlib
@@ -169,13 +170,49 @@ def _sd_keep(net, masks):
     return {bid: _t(masks[j]) > 0.5 for j, bid in enumerate(ids)}
 
 
-def _quorum_close(a, b, rtol, atol, frac=0.99, max_abs=None, what=""):
+# Per-element AdamW trajectory tolerance from the reference's own per-iteration gradients
+# (tests/golden/gen_golden_train.py records them as the optimizers see them).  The HIP
+# gradients equal autograd to 2e-3 of max|g| (test_*_gradients_match_autograd), so an element
+# whose reference gradient exceeds DECISIVE x max|g| in every iteration takes the same
+# sign-like AdamW steps as the reference: |p_hip - p_ref| <= TIGHT * lr per step (+ 1e-5 of
+# |p|).  Any other element may take an opposite sign-like step: <= 2 lr per step.  Every
+# element is bounded; none is excused by a quorum.
+DECISIVE, TIGHT = 0.02, 0.15
+
+
+def _ref_grads(rec, pname, upto=None):
+    gs, i = [], 0
+    while f"grad{i}/{pname}" in rec:
+        gs.append(_t(rec[f"grad{i}/{pname}"]).double())
+        i += 1
+    return gs if upto is None else gs[:upto]
+
+
+def _trajectory_close(a, b, grads, lr, what, tally=None):
+    a = a.detach().cpu().double().flatten()
+    b = b.detach().cpu().double().flatten()
+    n = min([a.numel(), b.numel()] + [g.numel() for g in grads])
+    a, b = a[:n], b[:n]
+    dec = torch.ones(n, dtype=torch.bool)
+    for g in grads:
+        g = g.flatten()[:n]
+        dec &= g.abs() > DECISIVE * max(g.abs().max().item(), 1e-30)
+    steps = len(grads)
+    tol = torch.where(dec, TIGHT * lr * steps + 1e-5 * b.abs() + 1e-7,
+                      torch.full_like(b, 2.0 * lr * steps * 1.001 + 1e-7))
+    d = (a - b).abs()
+    bad = d > tol
+    assert not bool(bad.any()), (f"{what}: {int(bad.sum())} / {n} elements beyond the AdamW step tolerance "
+                                 f"({int((bad & dec).sum())} decisive; max excess {float((d - tol).max()):.3g})")
+    if tally is not None:
+        tally[0] += int(dec.sum())
+        tally[1] += n
+
+
+def _moment_close(a, b, what, rel=5e-3):
+    """AdamW moments are smooth in the gradients: elementwise within rel of the tensor's scale."""
     a, b = a.detach().cpu().double(), b.detach().cpu().double()
-    ok = (a - b).abs() <= atol + rtol * b.abs()
-    assert ok.float().mean().item() >= frac, \
-        f"{what}: {(~ok).sum().item()} / {ok.numel()} elements differ (max |diff| {(a - b).abs().max().item():.3g})"
-    if max_abs is not None:
-        assert (a - b).abs().max().item() <= max_abs, what
+    torch.testing.assert_close(a, b, rtol=1e-3, atol=rel * b.abs().max().item() + 1e-12, msg=what)
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -186,7 +223,8 @@ def test_finetune_iterations_match_reference(gpu, name):
     lr_max = meta["lr"]
     for i, (xs1, xs2, ys) in enumerate(batches):
         if f"s{i}_w" in rec:      # the weights this iteration's forward saw
-            _quorum_close(cls.weight, _t(rec[f"s{i}_w"]), 1e-4, 1e-5, max_abs=4 * lr_max * i + 1e-6)
+            _trajectory_close(cls.weight, _t(rec[f"s{i}_w"]), _ref_grads(rec, "_classification.weight", i), lr_max,
+                              f"weight before iteration {i}")
         sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
         proto, pooled, out = T.train_forward_hip(net, torch.cat([xs1, xs2]).to(gpu), sd_keep)
         torch.testing.assert_close(pooled.cpu(), _t(rec[f"s{i}_pooled"]), rtol=1e-3, atol=2e-4)
@@ -200,18 +238,21 @@ def test_finetune_iterations_match_reference(gpu, name):
         assert float(stats[3]) == pytest.approx(comp["loss"], rel=1e-3, abs=1e-4)
         sched.step(0 + i / iters)
     assert [pytest.approx(x) for x in meta["info"]["lrs_class"][-1:]] == [sched.get_last_lr()[0]]
-    bound = 4 * lr_max * iters + 1e-6
     st = opt.state[cls.weight]
     assert float(st["step"]) == meta["steps"]
+    gw = _ref_grads(rec, "_classification.weight")
+    tally = [0, 0]
     if "final_w" in rec:
-        _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, max_abs=bound)
-        _quorum_close(st["exp_avg"], _t(rec["final_w_exp_avg"]), 1e-3, 1e-7)
-        _quorum_close(st["exp_avg_sq"], _t(rec["final_w_exp_avg_sq"]), 1e-3, 1e-10)
+        _trajectory_close(cls.weight, _t(rec["final_w"]), gw, lr_max, "final weight", tally)
+        _moment_close(st["exp_avg"], _t(rec["final_w_exp_avg"]), "exp_avg")
+        _moment_close(st["exp_avg_sq"], _t(rec["final_w_exp_avg_sq"]), "exp_avg_sq", rel=1e-2)
     else:
-        _quorum_close(cls.weight[:8], _t(rec["final_w_rows8"]), 1e-4, 1e-5, max_abs=bound)
-        _quorum_close(st["exp_avg"][:8], _t(rec["final_w_exp_avg_rows8"]), 1e-3, 1e-7)
+        _trajectory_close(cls.weight[:8], _t(rec["final_w_rows8"]), gw, lr_max, "final weight", tally)
+        _moment_close(st["exp_avg"][:8], _t(rec["final_w_exp_avg_rows8"]), "exp_avg")
     if cls.bias is not None:
-        _quorum_close(cls.bias, _t(rec["final_b"]), 1e-4, 1e-5, frac=0.9, max_abs=bound)
+        _trajectory_close(cls.bias, _t(rec["final_b"]), _ref_grads(rec, "_classification.bias"), lr_max,
+                          "final bias", tally)
+    assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
     assert float(cls.normalization_multiplier[0]) == pytest.approx(float(rec["final_mult"][0]))
 
 
@@ -318,12 +359,13 @@ def test_suffix_training_matches_reference(gpu, name):
             sched_cls.step(0 + i / iters)
         sched_net.step()
     # every trainable backbone / add-on tensor: sums, and the first 256 values elementwise
-    # (99 % quorum: AdamW's first steps move each weight by ~lr * sign(grad))
+    # within the per-element AdamW trajectory tolerance (_trajectory_close)
     names = [k.split("/")[1] for k in rec if k.startswith("param/") and k.endswith("/sum")]
     assert names
     params = dict(net.named_parameters())
     lr_max = max(g["lr"] for g in opt_net.param_groups) * 1.0
     resnet = fwd_meta["case"]["net"].startswith("resnet")
+    tally = [0, 0]
     for pname in names:
         p = params[pname].detach().cpu().double()
         head = _t(rec[f"param/{pname}/head"]).double()
@@ -335,8 +377,8 @@ def test_suffix_training_matches_reference(gpu, name):
             bound = 2.0 * meta["iterations"] * max(lr_p, meta["lr_net"], meta["lr_block"]) * 1.001 + 1e-7
             assert (p.flatten()[:head.numel()] - head).abs().max().item() <= bound, pname
             continue
-        _quorum_close(p.flatten()[:head.numel()], head, 1e-4, 1e-6, frac=0.95,
-                      max_abs=2.5 * meta["iterations"] * 10 * meta["lr_block"] + 1e-6, what=pname)
+        lr_p = next(g["lr"] for g in opt_net.param_groups if any(q is params[pname] for q in g["params"]))
+        _trajectory_close(p, head, _ref_grads(rec, pname), lr_p, pname, tally)
         ref_abs = float(rec[f"param/{pname}/abs"])
         assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
     _check_running_stats(net, rec)
@@ -347,12 +389,11 @@ def test_suffix_training_matches_reference(gpu, name):
         w8 = _t(rec["final_w_rows8"]).double()
         assert (cls.weight[:8].detach().cpu().double() - w8).abs().max().item() <= 2 * meta["lr"] * iters * 1.001
     elif not pretrain:
-        if "final_w" in rec:
-            _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, frac=0.97,
-                          max_abs=4 * meta["lr"] * iters + 1e-6)
-        else:
-            _quorum_close(cls.weight[:8], _t(rec["final_w_rows8"]), 1e-4, 1e-5, frac=0.97,
-                          max_abs=4 * meta["lr"] * iters + 1e-6)
+        w = _t(rec["final_w"]) if "final_w" in rec else _t(rec["final_w_rows8"])
+        _trajectory_close(cls.weight[:w.shape[0]], w, _ref_grads(rec, "_classification.weight"), meta["lr"],
+                          "classifier weight", tally)
+    if not resnet:
+        assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
 
 
 def _check_running_stats(net, rec):
@@ -494,7 +535,7 @@ def test_count_finetune_iterations_match_reference(gpu, name):
     """The reference's own train_pipnet(finetune=True, is_count_pipnet=True) run, replayed on
     the HIP step with its stochastic-depth masks and Gumbel noise: soft Gumbel map, raw counts
     and logits of every forward, the loss terms, and the classifier / intermediate tensors
-    after the run (99 % / 95 % elementwise quorum: AdamW's first steps move each weight by
+    after the run (per-element AdamW trajectory tolerance, _trajectory_close: AdamW moves each weight by
     ~lr * sign(grad), so a gradient near 0 may take either sign)."""
     from count_pipnet_amd.synthetic import synth_exponential
     meta, rec, fwd_meta, net, opt, sched, batches = _count_setup(name, gpu)
@@ -521,16 +562,19 @@ def test_count_finetune_iterations_match_reference(gpu, name):
         assert float(stats[0]) == pytest.approx(comp["align"], rel=1e-3, abs=1e-4)
         assert float(stats[3]) == pytest.approx(comp["loss"], rel=1e-3, abs=1e-4)
         sched.step(0 + i / iters)
-    bound = 4 * meta["lr"] * iters + 1e-6
     cls = net._classification
-    _quorum_close(cls.weight, _t(rec["final_w"]), 1e-4, 1e-5, max_abs=bound)
-    _quorum_close(opt.state[cls.weight]["exp_avg"], _t(rec["final_w_exp_avg"]), 1e-3, 1e-7)
+    tally = [0, 0]
+    _trajectory_close(cls.weight, _t(rec["final_w"]), _ref_grads(rec, "_classification.weight"), meta["lr"],
+                      "classifier weight", tally)
+    _moment_close(opt.state[cls.weight]["exp_avg"], _t(rec["final_w_exp_avg"]), "exp_avg")
     assert float(cls.normalization_multiplier[0]) == pytest.approx(float(rec["final_mult"][0]))
     inter = dict(net._intermediate.named_parameters())
     keys = [k for k in rec if k.startswith("inter/")]
     assert sorted(k[6:] for k in keys) == sorted(inter)
     for k in keys:
-        _quorum_close(inter[k[6:]], _t(rec[k]), 1e-4, 1e-5, frac=0.95, max_abs=bound)
+        lr_k = next(g["lr"] for g in opt.param_groups if any(q is inter[k[6:]] for q in g["params"]))
+        _trajectory_close(inter[k[6:]], _t(rec[k]), _ref_grads(rec, "_intermediate." + k[6:]), lr_k, k, tally)
+    assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
 
 
 def test_count_train_pipnet_epoch(gpu):
@@ -601,16 +645,19 @@ def test_count_suffix_training_matches_reference(gpu, name):
     assert sorted(names) == sorted(n for n, p in params.items() if p.requires_grad
                                    and not n.startswith("_classification"))
     lr_max = max(g["lr"] for g in opt_net.param_groups + opt_cls.param_groups)
+    tally = [0, 0]
     for pname in names:
         p = params[pname].detach().cpu().double()
         head = _t(rec[f"param/{pname}/head"]).double()
-        _quorum_close(p.flatten()[:head.numel()], head, 1e-4, 1e-6, frac=0.95,
-                      max_abs=2.5 * meta["iterations"] * lr_max + 1e-6)
+        lr_p = next(g["lr"] for g in opt_net.param_groups + opt_cls.param_groups
+                    if any(q is params[pname] for q in g["params"]))
+        _trajectory_close(p, head, _ref_grads(rec, pname), lr_p, pname, tally)
         ref_abs = float(rec[f"param/{pname}/abs"])
         assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
     if not pretrain:
-        _quorum_close(net._classification.weight, _t(rec["final_w"]), 1e-4, 1e-5, frac=0.97,
-                      max_abs=4 * meta["lr"] * iters + 1e-6)
+        _trajectory_close(net._classification.weight, _t(rec["final_w"]), _ref_grads(rec, "_classification.weight"),
+                          meta["lr"], "classifier weight", tally)
+    assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
 
 
 @pytest.mark.parametrize("name", COUNT_SUFFIX)
