@@ -100,10 +100,14 @@ def test_stem(gpu, bsz, h, wd):
     assert torch.allclose(out, ref, rtol=1e-4, atol=1e-4), (out - ref).abs().max()
 
 
-@pytest.mark.parametrize("c,h", [(96, 56), (192, 28), (384, 27), (768, 26), (768, 13), (384, 14), (96, 16), (192, 8)])
-def test_dwconv7_ln(gpu, c, h):
-    g = torch.Generator().manual_seed(c + h)
-    x, w, b = _rand(2, c, h, h, gen=g), _rand(c, 1, 7, 7, gen=g, scale=0.2), _rand(c, gen=g)
+@pytest.mark.parametrize("c,h,ww", [(96, 56, 56), (192, 28, 28), (384, 27, 27), (768, 26, 26), (768, 13, 13),
+                                    (384, 14, 14), (96, 16, 16), (192, 8, 8),
+                                    # small-map tiles (W <= 32 / 16): exact, ragged and non-square maps
+                                    (96, 32, 32), (96, 13, 29), (96, 33, 30), (192, 16, 16), (192, 11, 7),
+                                    (192, 20, 15)])
+def test_dwconv7_ln(gpu, c, h, ww):
+    g = torch.Generator().manual_seed(c + h + 7 * ww)
+    x, w, b = _rand(2, c, h, ww, gen=g), _rand(c, 1, 7, 7, gen=g, scale=0.2), _rand(c, gen=g)
     lw, lb = 1 + 0.1 * _rand(c, gen=g), 0.1 * _rand(c, gen=g)
     y = F.conv2d(x, w, b, padding=3, groups=c).permute(0, 2, 3, 1)
     ref = F.layer_norm(y, (c,), lw, lb, 1e-6)

@@ -17,6 +17,9 @@ extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, c
   V(5, 96, 7, 1, 1, 8) V(5, 192, 7, 1, 1, 16) V(5, 384, 7, 1, 2, 32) V(5, 768, 13, 1, 1, 64)
   V(6, 96, 7, 1, 2, 8) V(6, 192, 7, 1, 2, 16) V(6, 384, 14, 1, 1, 32) V(6, 768, 7, 1, 2, 64)
   V(7, 96, 14, 1, 1, 8) V(7, 192, 14, 1, 1, 16) V(7, 384, 7, 2, 1, 32) V(7, 768, 13, 1, 2, 64)
+  // v8-v10: narrower column tiles for small maps (a row tile of G * TX pixels against W = 32 / 16)
+  V(8, 96, 4, 1, 1, 8) V(8, 192, 4, 1, 1, 16) V(9, 96, 4, 2, 1, 8) V(9, 192, 4, 2, 1, 16)
+  V(10, 96, 2, 2, 1, 8) V(10, 192, 2, 2, 1, 16)
   R(1, 96, 4, 4, 2, 16) R(2, 96, 2, 4, 3, 16) R(3, 96, 4, 8, 1, 16) R(4, 96, 3, 4, 2, 16)
   R(1, 192, 4, 2, 2, 16) R(2, 192, 2, 2, 3, 16) R(3, 192, 4, 4, 1, 16) R(4, 192, 3, 2, 2, 16)
   R(1, 384, 4, 1, 2, 32) R(2, 384, 2, 1, 3, 32) R(3, 384, 4, 2, 1, 32) R(4, 384, 3, 1, 2, 32)

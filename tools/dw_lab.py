@@ -17,14 +17,19 @@ lib.lab_dw.argtypes = [I32, P, I32, I32, I32, I32, P, P, P, P, P, P, I32, I32]
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream().cuda_stream
 CHUNKS = [(2048, 7), (1024, 7), (4096, 4), (512, 14)]
-for c, hw in [(96, 56), (192, 28), (384, 27), (768, 26), (96, 32), (192, 16)]:
+SHAPES = [(96, 56), (192, 28), (384, 27), (768, 26), (96, 32), (192, 16)]
+if os.environ.get("DW_SHAPES"):
+    SHAPES = [tuple(int(v) for v in t.split("x")) for t in os.environ["DW_SHAPES"].split(",")]
+VARIANTS = [int(v) for v in os.environ.get("DW_VARIANTS", "0,5,6,7").split(",")]
+for c, hw in SHAPES:
     x = torch.randn(64, hw, hw, c, device=dev)
     w = torch.randn(49, c, device=dev) * 0.2
     b, lw, lb = torch.randn(c, device=dev), torch.randn(c, device=dev), torch.randn(c, device=dev)
     y = torch.empty_like(x)
     ref = None
     res = {}
-    combos = [(0, 2048, 7), (5, 2048, 7), (6, 2048, 7), (7, 2048, 7)] + [(v, mw, mr) for v in (1, 3) for mw, mr in CHUNKS[:2]]
+    combos = [(v, 2048, 7) for v in VARIANTS] + ([(v, mw, mr) for v in (1, 3) for mw, mr in CHUNKS[:2]]
+                                                 if os.environ.get("DW_RING") else [])
     for rnd in range(3):
         for v, mw, mr in combos:
             args = (v, x.data_ptr(), 64, hw, hw, c, w.data_ptr(), b.data_ptr(), lw.data_ptr(), lb.data_ptr(),
