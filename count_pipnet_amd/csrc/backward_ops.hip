@@ -157,12 +157,22 @@ __global__ __launch_bounds__(256) void colsum_finish_kernel(const float* __restr
   out[n] = accumulate ? out[n] + s : s;
 }
 
+// Slabs over the pixel rows: the fewest slabs s within 3 % of the minimum of the workgroup
+// rounds per unit of work, ceil(tiles * s / 512) / s (2 workgroups per CU), every slab >= 8
+// K-tiles.  (The
+// earlier ceil(512 / tiles) overshot 512 workgroups by a few -- 36 tiles x 15 = 540 -- and paid
+// a whole second round for them: the ResNet 3x3 weight gradients ran at ~40 TF/s.)
 int wgrad_splits(int M, int N1, int N2) {
   const int tiles = ((N1 + WB1 - 1) / WB1) * ((N2 + WB2 - 1) / WB2);
   const int ktiles = (M + WBK - 1) / WBK;
-  int s = (512 + tiles - 1) / tiles;                   // >= 2 workgroups per CU
-  s = s < ktiles / 8 ? s : ktiles / 8;                 // every slab >= 8 K-tiles
-  return s < 1 ? 1 : (s > 256 ? 256 : s);
+  const int smax = ktiles / 8 < 256 ? ktiles / 8 : 256;
+  auto cost = [&](int s) { return (double)(((int64_t)tiles * s + 511) / 512) / s; };
+  double best_cost = 1e30;
+  for (int s = 1; s <= smax; ++s) best_cost = cost(s) < best_cost ? cost(s) : best_cost;
+  // the fewest slabs within 3 % of the best (each slab adds an N1 x N2 partial to reduce)
+  for (int s = 1; s <= smax; ++s)
+    if (cost(s) <= best_cost * 1.03) return s;
+  return 1;
 }
 
 }  // namespace
