@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--torch-steps", type=int, default=3)
+    ap.add_argument("--phases", default="joint,finetune")
+    ap.add_argument("--hip-only", action="store_true", help="skip the torch-path timing (profiling runs)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
@@ -65,7 +67,7 @@ def main():
     ys = torch.randint(0, 200, (a.batch,), generator=g).to(dev)
     imgs = 2 * a.batch
     out = {}
-    for phase in ("joint", "finetune"):
+    for phase in a.phases.split(","):
         net, opt, opt_net = build(dev, phase == "joint")
         if phase == "joint":
             hip_s = timed(lambda: T.hip_train_step(net, xs1, xs2, ys, opt_net, opt, False, 1, 1, True), a.steps,
@@ -74,6 +76,9 @@ def main():
             hip_s = timed(lambda: T.hip_finetune_step(net, xs1, xs2, ys, opt, True), a.steps, a.warmup)
         del net, opt, opt_net
         torch.cuda.empty_cache()
+        if a.hip_only:
+            print(json.dumps({"phase": phase, "hip_ms_per_iter": hip_s * 1e3}), flush=True)
+            continue
         net, opt, opt_net = build(dev, phase == "joint")
         if phase == "joint":
             torch_s = timed(lambda: torch_joint_step(net, opt, opt_net, xs1, xs2, ys), a.torch_steps, 1)
