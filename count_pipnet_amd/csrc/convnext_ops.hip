@@ -204,7 +204,8 @@ extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, con
 // registers, full-line stores (tools/dw_lab.hip, profiles/r02/dw_lab.txt: 64 -> 63 / 37 -> 35 /
 // 59 -> 56 / 90 -> 85 us at the C2 stages).  Small maps take narrower column tiles (a row tile of
 // G * 7 pixels left 43 % of the lanes idle at W = 32 / 16): C5 stage 1 36.7 -> 26.2 us, stage 2
-// 18.2 -> 16.9 us; the choice depends on W only (per-pixel results stay batch-invariant).
+// 18.2 -> 16.9 us; at C1's 16^2 / 8^2 maps (batch 16) the wide tile stays 2 % faster, hence the
+// lower bounds.  The choice depends on W only (per-pixel results stay batch-invariant).
 extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C, const float* w_packed,
                                      const float* bias, const float* ln_w, const float* ln_b, float* y,
                                      void* stream) {
@@ -217,10 +218,10 @@ extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C,
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
     case 96:
-      if (W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<96, 7, 1, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192:
-      if (W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<192, 7, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, false, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
@@ -239,10 +240,10 @@ extern "C" int pipnet_dwconv7_ln_s3(const float* x, int B, int H, int W, int C, 
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
     case 96:
-      if (W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<96, 7, 1, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192:
-      if (W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<192, 7, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, true, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
