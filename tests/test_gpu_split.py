@@ -80,7 +80,7 @@ def test_conv_s3_matches_split_product(gpu, b, h, cin, cout, kh, stride, tile, e
     assert torch.all((got - exact).abs() <= 3e-5 * scale_ + tol)
 
 
-@pytest.mark.parametrize("b,h,c", [(2, 9, 96), (1, 8, 192), (2, 7, 384), (1, 6, 768)])
+@pytest.mark.parametrize("b,h,c", [(2, 9, 96), (1, 8, 192), (2, 7, 384), (1, 6, 768), (2, 24, 96), (1, 12, 192)])
 def test_dwconv7_ln_s3_is_split_of_fp32_kernel(gpu, b, h, c):
     g = torch.Generator().manual_seed(c + h)
     x = torch.randn(b, h, h, c, generator=g).to(gpu)
