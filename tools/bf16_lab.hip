@@ -342,6 +342,140 @@ __global__ __launch_bounds__(pp::NT, 1) void lab_prs_kernel(ConvParams p) {
 }
 }  // namespace pipnet_bf16
 
+namespace pipnet_bf16 {
+// Lab-only: register staging two K-tiles deep.  Same LDS schedule as lab_prs_kernel (B(t+2)
+// written in phase 0 of K-tile t, A(t+3) in phase 1), but each piece is LOADED two K-tiles
+// before its write (B(t+4) / A(t+5) issued in K-tile t) into a register ring of two slots,
+// so a global load has two K-tiles (~4 MFMA phases of both groups) to land.  The K loop is
+// unrolled by two so the ring slot is a compile-time register.  Dense A only.
+template <int ABL>
+__global__ __launch_bounds__(pp::NT, 1) void lab_prs2_kernel(ConvParams p) {
+  using namespace pp;
+  constexpr int NS = 4, NB = 4, WCOLS = 64;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[smem_bytes<2>()];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  int m0, n0;
+  tile_coords(p, BM, 4 * WCOLS, m0, n0);
+  const int nk = p.K / BK;
+  const int drow = lane >> 2;
+  const int dchunk = 8 * ((lane & 3) ^ g(drow));
+  const bf16* asrc[2];
+  const bf16* wsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * (wid + 8 * i) + drow;
+    asrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + dchunk;
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
+  }
+  bf16x8v ra[2][2], rb[2][2];                 // [ring slot][piece]
+  auto load_a = [&](int kt, bf16x8v (&r)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = *reinterpret_cast<const bf16x8v*>(asrc[i] + (kt < nk ? kt : 0) * BK);
+  };
+  auto load_b = [&](int kt, bf16x8v (&r)[2]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) r[i] = *reinterpret_cast<const bf16x8v*>(wsrc[i] + (kt < nk ? kt : 0) * BK);
+  };
+  auto write_a = [&](int kt, const bf16x8v (&r)[2]) {
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<bf16x8v*>(base + (wid + 8 * i) * 1024 + lane * 16) = r[i];
+  };
+  auto write_b = [&](int kt, const bf16x8v (&r)[2]) {
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES + BM * ROWB;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<bf16x8v*>(base + (wid + 8 * i) * 1024 + lane * 16) = r[i];
+  };
+  const int fr = lane & 15;
+  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
+  };
+  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * WCOLS + n * 16) * ROWB + fofs);
+  };
+  f32x4v acc[8][NB];
+#pragma unroll
+  for (int r = 0; r < 8; ++r)
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  // prologue: tiles 0, 1 (A and B) and A(2) in LDS; ring: B(2) B(3) and A(3) A(4) in flight
+  {
+    bf16x8v t[2];
+    for (int k = 0; k < 2 && k < nk; ++k) {
+      load_a(k, t); write_a(k, t);
+      load_b(k, t); write_b(k, t);
+    }
+    if (2 < nk) { load_a(2, t); write_a(2, t); }
+  }
+  load_b(2, rb[0]);
+  load_b(3, rb[1]);
+  load_a(3, ra[0]);
+  load_a(4, ra[1]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (wr == 1) pp_barrier();
+  bf16x8v fa[4], fb[4];
+  auto ktile = [&](int kt, auto slotc) {
+    constexpr int S = decltype(slotc)::value;
+    const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+    if (kt + 2 < nk) write_b(kt + 2, rb[S]);             // loaded two K-tiles ago
+    load_b(kt + 4, rb[S]);                               // (clamped past nk: harmless reload)
+    read_b(fb, st);
+    read_a(fa, st, 0);
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+    if (kt + 3 < nk) write_a(kt + 3, ra[S]);
+    load_a(kt + 5, ra[S]);
+    read_a(fa, st, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    pp_barrier();
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    ktile(kt, IntC<0>{});
+    ktile(kt + 1, IntC<1>{});
+  }
+  if (kt < nk) ktile(kt, IntC<0>{});
+  if (wr == 0) pp_barrier();
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  pp_barrier();
+  if constexpr ((ABL & 2) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += acc[r][n][i];
+    reinterpret_cast<float*>(p.C)[(int64_t)blockIdx.x * pp::NT + tid] = t;
+    return;
+  }
+  pp_epilogue<PIPNET_EPI_NONE, 4>(p, acc, smem, m0, n0, wr, wc, lane, wid);
+}
+}  // namespace pipnet_bf16
+
 namespace {
 int group_for(int K, double budget) {
   const double panel = 128.0 * K * 2.0;
@@ -377,6 +511,8 @@ extern "C" int lab_pp(int abl, const void* A, const void* W, void* C, int M, int
   switch (abl) {
     case 256: hipLaunchKernelGGL((lab_prs_kernel<0>), grid, dim3(512), 0, s, p); break;
     case 258: hipLaunchKernelGGL((lab_prs_kernel<2>), grid, dim3(512), 0, s, p); break;
+    case 512: hipLaunchKernelGGL((lab_prs2_kernel<0>), grid, dim3(512), 0, s, p); break;
+    case 514: hipLaunchKernelGGL((lab_prs2_kernel<2>), grid, dim3(512), 0, s, p); break;
     LAB_CP(0, 0, 0) LAB_CP(1, 1, 1) LAB_CP(2, 2, 2) LAB_CP(3, 16, 16) LAB_CP(4, 17, 17) LAB_CP(5, 2, 0)
     LAB_CP(6, 0, 2) LAB_CP(7, 3, 3) LAB_CP(8, 16, 0) LAB_CP(9, 0, 16)
     LAB_P64(0) LAB_P64(1) LAB_P64(2) LAB_P64(4) LAB_P64(8) LAB_P64(16) LAB_P64(18) LAB_P64(32) LAB_P64(34)
