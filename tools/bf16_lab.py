@@ -53,7 +53,7 @@ def main():
         c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         res = {}
         # correctness: the full-line kernel accumulates in the same k order as the 32-deep one
-        for alt in (32, 256, 512):
+        for alt in (32, 256, 512, 1024):
             if alt not in abls or 0 not in abls:
                 continue
             c2 = torch.empty_like(c)
