@@ -1,7 +1,7 @@
 // Tuning lab for the depthwise 7x7 + LayerNorm kernel (not part of the product ABI):
-// v0 = the register-tile kernel (convnext_dw.hpp), v1.. = row-ring variants (convnext_dw_ring.hpp).
+// v0 = the register-tile kernel (convnext_dw.hpp), v1.. = row-ring variants (dw_ring_lab.hpp).
 #include "../count_pipnet_amd/csrc/convnext_dw.hpp"
-#include "../count_pipnet_amd/csrc/convnext_dw_ring.hpp"
+#include "dw_ring_lab.hpp"
 using namespace pipnet_dw;
 
 extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, const float* wp, const float* bias,

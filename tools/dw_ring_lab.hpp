@@ -1,5 +1,5 @@
-// depthwise 7x7 + LayerNorm(C), row-ring formulation (shared by convnext_ops.hip and
-// tools/dw_lab.hip).
+// depthwise 7x7 + LayerNorm(C), row-ring formulation -- LAB ONLY (tools/dw_lab.hip); the product
+// uses the register-tile kernel in count_pipnet_amd/csrc/convnext_dw.hpp.
 //
 // Each thread owns one channel pair (f32x2 -> v_pk_fma_f32) of a strip of TX adjacent output
 // columns and walks DOWN a chunk of output rows.  Its 49 weight pairs live in registers for
@@ -19,7 +19,7 @@
 #pragma once
 #include <algorithm>
 
-#include "common.hpp"
+#include "../count_pipnet_amd/csrc/common.hpp"
 
 namespace pipnet_dw {
 
