@@ -52,6 +52,7 @@ struct GemmParams {
   long long* stamps;      // lab (ABL & 8): per-workgroup s_memtime stamps + hardware ids
   const float* row_scale; // PIPNET_EPI_RESID_ROWSCALE: per row-group factor (stochastic depth)
   int rows_per_scale;
+  int xcd_ng;             // > 0: XCD-slab raster (tile_coords); 0: grouped raster
 };
 
 // Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 8
@@ -247,6 +248,16 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
   return x;
 }
 
+// Output-tile store.  PIPNET_GEMM_NT_STORE (A/B builds only): non-temporal stores, so the
+// streaming C tiles do not evict the A / W panels other workgroups of the XCD still read.
+PIPNET_DEV void st4_c(float* p, f32x4 v) {
+#if defined(PIPNET_GEMM_NT_STORE) && PIPNET_GEMM_NT_STORE
+  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+#else
+  st4(p, v);
+#endif
+}
+
 // Vectorised epilogue: each wave re-lays its accumulator tile through LDS (32 rows at a
 // time, 8 KiB per wave) so every global store / residual load is a float4 and one wave
 // instruction covers 4 rows x 256 B -- the lane-per-column MFMA layout would otherwise
@@ -293,13 +304,29 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, i
       float rs = 1.f;
       if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
       const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
-      if (m < p.M && nok) st4(p.C + (int64_t)m * p.ldc + n, x);
+      if (m < p.M && nok) st4_c(p.C + (int64_t)m * p.ldc + n, x);
     }
   }
 }
 
 // XCD-contiguous tile ranges, group_m-grouped raster (m fastest inside a group).
-PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
+// xcd_ng > 0 (XCD-slab raster): XCD x (= blockIdx % 8 under round-robin dispatch) owns the
+// N-panels [x % ng]-th of ng slabs and the M-rows (x / ng)-th of 8 / ng slabs, walked N-fastest,
+// so its W slab stays L2-resident and each A panel is fetched by ng XCDs in total.  The grid
+// is 8 x the largest slab; workgroups past their slab return false (uniformly, before any
+// barrier).
+PIPNET_DEV bool tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
+  if (p.xcd_ng > 0) {
+    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
+    const int ng = p.xcd_ng, mg = 8 / ng;
+    const int xn = x % ng, xm = x / ng;
+    const int nb0 = xn * p.nt / ng, nr = (xn + 1) * p.nt / ng - nb0;
+    const int mb0 = xm * p.mt / mg, mr = (xm + 1) * p.mt / mg - mb0;
+    if (nr <= 0 || l >= mr * nr) return false;
+    m0 = (mb0 + l / nr) * bm;
+    n0 = (nb0 + l % nr) * BN;
+    return true;
+  }
   const int nwg = p.mt * p.nt;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int gm = p.group_m;
@@ -309,6 +336,7 @@ PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int in_group = tile - group * gm * p.nt;
   m0 = (first_m + in_group % gsz) * bm;
   n0 = (in_group / gsz) * BN;
+  return true;
 }
 
 PIPNET_DEV void zero_acc(Acc& acc) {
@@ -413,7 +441,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   const int wm = wid >> 1, wn = NPAD ? ((wid & 1) ^ (int)(blockIdx.x & 1)) : (wid & 1);
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, G::BMT, m0, n0);
+  if (!tile_coords(p, G::BMT, m0, n0)) return;
   const int jl = NPAD ? __builtin_amdgcn_readfirstlane(min(2, max(0, (p.N - n0 - wn * 64 + 31) >> 5))) : 2;
   if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
@@ -544,7 +572,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
   const int wm = wid >> 1, wn = wid & 1;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, TBM, m0, n0);
+  if (!tile_coords(p, TBM, m0, n0)) return;
 
   const int srow = tid >> 3;
   const int sk = (tid & 7) * 4;
