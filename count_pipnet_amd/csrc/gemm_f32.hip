@@ -1,6 +1,4 @@
 // Product instantiation of the fp32 MFMA GEMM (templates + design notes: gemm_f32_impl.hpp).
-#include <cstdlib>
-
 #include "gemm_f32_impl.hpp"
 
 using namespace pipnet_gemm;
@@ -17,17 +15,6 @@ int choose_group_m(const GemmParams& p) {
   int g = (int)(PIPNET_GROUP_BUDGET / panel);
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
-
-// XCD-slab raster (tile_coords): lab switch PIPNET_XCD_NG (env, A/B builds compiled with
-// -DPIPNET_XCD_NG_LAB): 0 = grouped raster, 1/2/4/8 = N slabs.
-#ifdef PIPNET_XCD_NG_LAB
-int xcd_slabs(const GemmParams& p, int v) {
-  static const int ng = getenv("PIPNET_XCD_NG") ? atoi(getenv("PIPNET_XCD_NG")) : 0;
-  return (v == 3 && p.mt * p.nt >= 1024 && ng > 0 && p.nt >= ng) ? ng : 0;
-}
-#else
-int xcd_slabs(const GemmParams&, int) { return 0; }
-#endif
 
 // Variant selection (measured with tools/gemm_lab.py on the network's shapes, MI355X,
 // float4 epilogue, profiles/r01/gemm_lab_*.txt):
@@ -74,10 +61,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
   const int v = gemm_variant(p.M, p.N, p.K, vec);
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
-  p.xcd_ng = xcd_slabs(p, v);
-  const dim3 grid(p.xcd_ng ? 8 * ((p.mt + 8 / p.xcd_ng - 1) / (8 / p.xcd_ng)) * ((p.nt + p.xcd_ng - 1) / p.xcd_ng)
-                           : p.mt * p.nt),
-      block(NTHREADS);
+  const dim3 grid(p.mt * p.nt), block(NTHREADS);
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
     if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \

@@ -52,7 +52,6 @@ struct GemmParams {
   long long* stamps;      // lab (ABL & 8): per-workgroup s_memtime stamps + hardware ids
   const float* row_scale; // PIPNET_EPI_RESID_ROWSCALE: per row-group factor (stochastic depth)
   int rows_per_scale;
-  int xcd_ng;             // > 0: XCD-slab raster (tile_coords); 0: grouped raster
 };
 
 // Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 8
@@ -248,15 +247,10 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
   return x;
 }
 
-// Output-tile store.  PIPNET_GEMM_NT_STORE (A/B builds only): non-temporal stores, so the
-// streaming C tiles do not evict the A / W panels other workgroups of the XCD still read.
-PIPNET_DEV void st4_c(float* p, f32x4 v) {
-#if defined(PIPNET_GEMM_NT_STORE) && PIPNET_GEMM_NT_STORE
-  __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
-#else
-  st4(p, v);
-#endif
-}
+// Output-tile store: non-temporal, so the streaming C tiles do not evict the A / W panels
+// other workgroups of the XCD still read (s384 fc1: 338 -> 184 MiB fetched per launch at
+// equal time, profiles/r02/gemm_raster_store_ab.txt).
+PIPNET_DEV void st4_c(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p)); }
 
 // Vectorised epilogue: each wave re-lays its accumulator tile through LDS (32 rows at a
 // time, 8 KiB per wave) so every global store / residual load is a float4 and one wave
@@ -309,24 +303,10 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, i
   }
 }
 
-// XCD-contiguous tile ranges, group_m-grouped raster (m fastest inside a group).
-// xcd_ng > 0 (XCD-slab raster): XCD x (= blockIdx % 8 under round-robin dispatch) owns the
-// N-panels [x % ng]-th of ng slabs and the M-rows (x / ng)-th of 8 / ng slabs, walked N-fastest,
-// so its W slab stays L2-resident and each A panel is fetched by ng XCDs in total.  The grid
-// is 8 x the largest slab; workgroups past their slab return false (uniformly, before any
-// barrier).
-PIPNET_DEV bool tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
-  if (p.xcd_ng > 0) {
-    const int x = blockIdx.x & 7, l = blockIdx.x >> 3;
-    const int ng = p.xcd_ng, mg = 8 / ng;
-    const int xn = x % ng, xm = x / ng;
-    const int nb0 = xn * p.nt / ng, nr = (xn + 1) * p.nt / ng - nb0;
-    const int mb0 = xm * p.mt / mg, mr = (xm + 1) * p.mt / mg - mb0;
-    if (nr <= 0 || l >= mr * nr) return false;
-    m0 = (mb0 + l / nr) * bm;
-    n0 = (nb0 + l % nr) * BN;
-    return true;
-  }
+// XCD-contiguous tile ranges, group_m-grouped raster (m fastest inside a group).  (An
+// XCD-slab raster -- each XCD owning an N slab so its W panels stay L2-resident -- measured no
+// faster, profiles/r02/gemm_raster_store_ab.txt.)
+PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int nwg = p.mt * p.nt;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int gm = p.group_m;
@@ -336,7 +316,6 @@ PIPNET_DEV bool tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int in_group = tile - group * gm * p.nt;
   m0 = (first_m + in_group % gsz) * bm;
   n0 = (in_group / gsz) * BN;
-  return true;
 }
 
 PIPNET_DEV void zero_acc(Acc& acc) {
@@ -441,7 +420,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   const int wm = wid >> 1, wn = NPAD ? ((wid & 1) ^ (int)(blockIdx.x & 1)) : (wid & 1);
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  if (!tile_coords(p, G::BMT, m0, n0)) return;
+  tile_coords(p, G::BMT, m0, n0);
   const int jl = NPAD ? __builtin_amdgcn_readfirstlane(min(2, max(0, (p.N - n0 - wn * 64 + 31) >> 5))) : 2;
   if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
@@ -572,7 +551,7 @@ __global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_ktail_kernel(GemmPara
   const int wm = wid >> 1, wn = wid & 1;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  if (!tile_coords(p, TBM, m0, n0)) return;
+  tile_coords(p, TBM, m0, n0);
 
   const int srow = tid >> 3;
   const int sk = (tid & 7) * 4;

@@ -1,4 +1,6 @@
 # A/B of the fp32 GEMM raster / store policy (lab builds tools/lib_xcdng.so, lib_ntstore.so):
+# (The XCD-slab raster and PIPNET_GEMM_NT_STORE switches exist at commit "fp32 GEMM lab switches"; NT stores
+# became the product default and the slab raster was removed in the commit after it.)
 # output digests (must match), gemm_bench timings, FETCH_SIZE per shape.
 set -u
 cd $GRAFT_REPO_ROOT
