@@ -119,10 +119,13 @@ class PIPNet(nn.Module):
         return nhwc_as_nchw(proto), (clamped if inference else pooled), out
 
 
-# Opt-in (set_stream_split(net, 2)): batches of at least this many images run as concurrent
-# sub-batches on n HIP streams -- ConvNeXt: +2.5 % images/s on BASELINE C2 (21.9 vs 22.4 ms,
-# tools/stream_overlap.py).  Off by default: per-kernel timings (bench.py's roofline, rocprof
-# averages) then mix two co-running launches, so the measured path stays one stream.
+# Concurrent sub-batches: batches of at least STREAM_SPLIT_MIN_BATCH images run as n
+# half-batch forwards on n HIP streams, so one half's tile-quantisation tails and
+# bandwidth-bound kernels co-run with the other half's MFMA tiles.  Default 2 for ResNet
+# backbones (C3 bs=128: bf16 15.3k -> 17.2k img/s, fp32 +3 %, profiles/r02/stream_split_c3.log;
+# 3 streams equal, 4 no gain), 1 for ConvNeXt, where it is opt-in (set_stream_split(net, 2):
+# +2.5 % on BASELINE C2) so bench.py's per-kernel roofline timings describe one launch, not
+# two co-running ones.
 STREAM_SPLIT_MIN_BATCH = 32
 _SIDE_STREAMS = {}
 
@@ -135,14 +138,18 @@ def _side_streams(dev, n):
 
 
 def set_stream_split(net: nn.Module, n: int) -> nn.Module:
-    """Number of concurrent sub-batch streams for the HIP forward (1 = off, the default).
-    Outputs are bit-identical either way (every kernel is batch-invariant)."""
+    """Number of concurrent sub-batch streams for the HIP forward (1 = off; default 2 for
+    ResNet backbones, 1 otherwise).  Outputs are bit-identical either way (every kernel is
+    batch-invariant)."""
     (net.module if hasattr(net, "module") else net)._hip_stream_split = int(n)
     return net
 
 
 def stream_split(model: nn.Module, xs: Tensor) -> int:
-    n = getattr(model, "_hip_stream_split", 1)
+    n = getattr(model, "_hip_stream_split", None)
+    if n is None:
+        from .resnet_features import ResNet_features
+        n = 2 if isinstance(getattr(model, "_net", None), ResNet_features) else 1
     if n <= 1 or xs.shape[0] < max(STREAM_SPLIT_MIN_BATCH, n):
         return 1
     return n

@@ -90,3 +90,22 @@ def test_stream_split_bit_identical_and_graph(gpu):
     torch.cuda.synchronize()
     for a, b in zip(outs, one):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_stream_split_resnet_default(gpu, dtype):
+    """ResNet backbones split batches >= 32 over 2 streams by default (C3: +12 % bf16);
+    bit-identical to the one-stream forward in both HIP dtypes."""
+    from count_pipnet_amd.pipnet import set_hip_dtype, set_stream_split, stream_split
+    from count_pipnet_amd.synthetic import synth_images
+    net, _, _ = _net("c3_pipnet_resnet50", gpu)
+    set_hip_dtype(net, dtype)
+    xs = synth_images(36, 64, seed=11).to(gpu)
+    assert stream_split(net, xs) == 2
+    assert stream_split(net, xs[:16]) == 1               # small batches stay on one stream
+    with torch.no_grad():
+        split = [t.clone() for t in net(xs, inference=True)]
+        set_stream_split(net, 1)
+        one = [t.clone() for t in net(xs, inference=True)]
+    for a, b in zip(split, one):
+        assert torch.equal(a, b)

@@ -6,7 +6,7 @@
   C2' PIP-Net ConvNeXt-tiny-13 224x224, bs=64          (the 13x13 variant)
   *_bf16x3: the same ConvNeXt configs with split-bf16 GEMMs (set_hip_dtype "bf16x3")
 
-    python tools/bench_configs.py [--steps 10] [--only c5]
+    python tools/bench_configs.py [--steps 10] [--only c5] [--stream-split 2]
 Prints one JSON line per config (images/sec, ms/step, model TFLOP/s where defined).
 """
 import argparse
@@ -22,7 +22,12 @@ import torch  # noqa: E402
 
 from count_pipnet_amd import build  # noqa: E402
 from count_pipnet_amd.count_pipnet import get_count_network  # noqa: E402
-from count_pipnet_amd.pipnet import get_pipnet  # noqa: E402
+from count_pipnet_amd.pipnet import get_pipnet, set_stream_split  # noqa: E402
+from count_pipnet_amd.pipnet import stream_split as _stream_split  # noqa: E402
+
+
+def split_of(net, xs):
+    return _stream_split(net, xs) if hasattr(net, "_hip_logits") else 1
 from count_pipnet_amd.synthetic import fill_module_, synth_images  # noqa: E402
 
 CONFIGS = {
@@ -63,6 +68,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--only", default=None)
     ap.add_argument("--graph", action="store_true", help="also time HIP-graph replay (count_pipnet_amd.graph)")
+    ap.add_argument("--stream-split", type=int, default=0,
+                    help="force pipnet.set_stream_split(net, n) on every config (0 = the model's default)")
     a = ap.parse_args()
     build.build()
     dev = torch.device("cuda:0")
@@ -70,6 +77,8 @@ def main():
         if a.only and name != a.only:
             continue
         net = make(cfg, dev)
+        if a.stream_split:
+            set_stream_split(net, a.stream_split)
         xs = synth_images(cfg["batch"], cfg["size"], seed=5).to(dev)
         with torch.no_grad():
             for _ in range(a.warmup):
@@ -87,7 +96,8 @@ def main():
         peak = {"bf16": 2500.0, "bf16x3": 2500.0 / 3.0}.get(dt, 157.3)
         rec = dict(config=name, images_per_sec=ips, ms_per_step=el / a.steps * 1e3, batch=cfg["batch"],
                    image_size=cfg["size"], dtype=dt, model_tflops=ips * cfg["gflop"] / 1e3,
-                   model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak)
+                   model_frac_of_peak=ips * cfg["gflop"] / 1e3 / peak, peak_tflops=peak,
+                   stream_split=split_of(net, xs))
         if a.graph:
             from count_pipnet_amd.graph import GraphedForward
             g = GraphedForward(net)
