@@ -23,7 +23,7 @@ from .backend import use_hip
 from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
 from .count_pipnet_utils import (BilinearIntermediate, ClampSTE, GumbelSoftmax, IdentityIntermediate,
                                  LinearFull, LinearIntermediate, OneHotEncoder, STE_Round)
-from .pipnet import add_on_logits_hip
+from .pipnet import _side_streams, add_on_logits_hip, stream_split
 
 
 class CountPIPNet(nn.Module):
@@ -66,6 +66,10 @@ class CountPIPNet(nn.Module):
     # -- HIP inference path ---------------------------------------------------------------
     def _forward_hip(self, xs, inference):
         K.require_device(xs, "input images")
+        n = stream_split(self, xs)
+        # (the Philox offset of a sub-batch, b0*h*w*P/4 blocks, is exact for P % 4 == 0)
+        if n > 1 and self._num_prototypes % 4 == 0 and not torch.cuda.is_current_stream_capturing():
+            return self._forward_hip_split(xs, inference, n)
         feats = as_nhwc(self._net(xs))
         act = list(self._add_on)[-1] if isinstance(self._add_on, nn.Sequential) else self._add_on
         do_round = bool(self._use_ste or inference)
@@ -87,6 +91,59 @@ class CountPIPNet(nn.Module):
             logits = add_on_logits_hip(self._add_on, feats, activation=nn.Softmax)
             proto, sums = K.softmax_pool(logits, pool_mode=1)
             counts, clamped = K.count_finish(None, sums, self._max_count, do_round)
+        inter = intermediate_hip(self._intermediate, clamped)
+        cls = self._classification
+        _, out = K.nonneg_linear(inter, cls.weight, cls.bias, None)
+        return nhwc_as_nchw(proto), (clamped if inference else counts), out
+
+    def _forward_hip_split(self, xs, inference, n):
+        """The backbone, add-on and count head of n sub-batches on n concurrent HIP streams
+        (pipnet.PIPNet._forward_hip_split), joined before the count -> classifier layers, which
+        run once on the whole batch (the Bilinear intermediate streams 352 MB of weights per
+        call).  Per-image results are batch-invariant and the Gumbel noise of sub-batch image
+        b0 starts at Philox block b0*h*w*P/4, so the outputs equal the one-stream forward's."""
+        dev = xs.device
+        main = torch.cuda.current_stream(dev)
+        streams = _side_streams(dev, n)
+        parts = xs.chunk(n)
+        act = list(self._add_on)[-1] if isinstance(self._add_on, nn.Sequential) else self._add_on
+        gumbel = isinstance(act, GumbelSoftmax)
+        logits = []
+        for s, p in zip(streams, parts):
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                feats = as_nhwc(self._net(p))
+                logits.append(add_on_logits_hip(self._add_on, feats,
+                                                activation=GumbelSoftmax if gumbel else nn.Softmax))
+        b = xs.shape[0]
+        _, h, w, pn = logits[0].shape
+        proto = torch.empty((b, h, w, pn), device=dev, dtype=torch.float32)
+        noise = seed = None
+        if gumbel:
+            hist = torch.empty((b, pn), device=dev, dtype=torch.int32)
+            noise = act.exp_noise
+            if noise is not None:
+                noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+            else:
+                seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+        else:
+            sums = torch.empty((b, pn), device=dev, dtype=torch.float32)
+        i0 = 0
+        for s, lg in zip(streams, logits):
+            i1 = i0 + lg.shape[0]
+            s.wait_stream(main)                            # outputs allocated on main before any write
+            with torch.cuda.stream(s):
+                if gumbel:
+                    K.count_gumbel(lg, act.tau, None if noise is None else noise[i0:i1], seed or 0,
+                                   offset=i0 * h * w * pn // 4, out=(proto[i0:i1], hist[i0:i1]))
+                else:
+                    K.softmax_pool(lg, pool_mode=1, out=(proto[i0:i1], sums[i0:i1]))
+            i0 = i1
+        for s in streams:
+            main.wait_stream(s)
+        do_round = bool(self._use_ste or inference)
+        counts, clamped = K.count_finish(hist if gumbel else None, None if gumbel else sums, self._max_count,
+                                         do_round)
         inter = intermediate_hip(self._intermediate, clamped)
         cls = self._classification
         _, out = K.nonneg_linear(inter, cls.weight, cls.bias, None)

@@ -494,16 +494,27 @@ def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional
 
 
 def count_gumbel(logits_nhwc: Tensor, tau: float, exp_noise_nchw: Optional[Tensor], seed: int,
-                 offset: int = 0) -> Tuple[Tensor, Tensor]:
-    """Hard Gumbel-softmax one-hot map [B,h,w,P] + int32 histogram [B,P]."""
+                 offset: int = 0, out=None) -> Tuple[Tensor, Tensor]:
+    """Hard Gumbel-softmax one-hot map [B,h,w,P] + int32 histogram [B,P].  ``offset`` (Philox
+    blocks) shifts the noise stream: image b0 of a batch starts at b0*h*w*P/4.  ``out`` =
+    (proto, hist) to write into (batch slices of a larger output)."""
     _chk(logits_nhwc, "prototype logits")
     b, h, w, p = logits_nhwc.shape
     if exp_noise_nchw is not None:
         _chk(exp_noise_nchw, "exp noise")
         if tuple(exp_noise_nchw.shape) != (b, p, h, w):
             raise RuntimeError(f"exp noise shape {tuple(exp_noise_nchw.shape)} != {(b, p, h, w)}")
-    proto = torch.empty_like(logits_nhwc)
-    hist = torch.empty((b, p), device=logits_nhwc.device, dtype=torch.int32)
+    if out is None:
+        proto = torch.empty_like(logits_nhwc)
+        hist = torch.empty((b, p), device=logits_nhwc.device, dtype=torch.int32)
+    else:
+        proto, hist = out
+        if tuple(proto.shape) != (b, h, w, p) or tuple(hist.shape) != (b, p) or hist.dtype != torch.int32:
+            raise RuntimeError(f"count_gumbel: out {tuple(proto.shape)}, {tuple(hist.shape)} {hist.dtype} do not "
+                               f"match {(b, h, w, p)}, {(b, p)} int32")
+        _chk(proto, "proto out")
+        if not (hist.is_cuda and hist.is_contiguous()):
+            raise RuntimeError("count_gumbel: hist out must be a contiguous device tensor")
     _lib.call("pipnet_count_gumbel_f32", logits_nhwc.data_ptr(), b, h * w, p, float(tau), _ptr(exp_noise_nchw),
               int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), proto.data_ptr(), hist.data_ptr(),
               _stream(logits_nhwc))

@@ -109,3 +109,27 @@ def test_stream_split_resnet_default(gpu, dtype):
         one = [t.clone() for t in net(xs, inference=True)]
     for a, b in zip(split, one):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("noise", ["injected", "philox"])
+def test_count_stream_split_bit_identical(gpu, noise):
+    """CountPIPNet split forward (backbone + Gumbel head per sub-batch stream, count layers on
+    the whole batch) == the one-stream forward: injected noise sliced per sub-batch, Philox
+    noise offset to the sub-batch's first image."""
+    from count_pipnet_amd.pipnet import set_stream_split, stream_split
+    from count_pipnet_amd.synthetic import synth_exponential, synth_images
+    net, _, _ = _net("c1_count_identity", gpu)
+    xs = synth_images(40, 64, seed=13).to(gpu)
+    act = list(net._add_on)[-1]
+    b, p = xs.shape[0], net._num_prototypes
+    act.exp_noise = synth_exponential((b, p, 8, 8), seed=6).to(gpu) if noise == "injected" else None
+    outs = {}
+    with torch.no_grad():
+        for n in (1, 2, 3):
+            set_stream_split(net, n)
+            assert stream_split(net, xs) == n
+            torch.manual_seed(1234)                      # same Philox key for every variant
+            outs[n] = [t.clone() for t in net(xs, inference=True)]
+    for n in (2, 3):
+        for a, r in zip(outs[n], outs[1]):
+            assert torch.equal(a, r)
