@@ -444,13 +444,38 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     const int c = G::swz(row, lane % G::CHUNKS);
     wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 4 * c;
   }
+  // Implicit-GEMM convolutions with Cin % BK == 0: a K-tile never straddles two taps, so the
+  // (channel, kx, ky) of the next K-tile the DMA fetches is tracked incrementally (stage() is
+  // called for consecutive K-tiles) -- wave-uniform, no per-lane division in the loop.
+  const bool tap_walk = ALOAD != ALOAD_DENSE && p.Cin % BK == 0;
+  int t_c = 0, t_kx = 0, t_ky = 0;
+  if (ALOAD != ALOAD_DENSE && tap_walk) {
+    const int k = kt_begin * BK, tap = k / p.Cin;
+    t_c = k - tap * p.Cin;
+    t_ky = ALOAD == ALOAD_CONV2X2 ? tap >> 1 : tap / p.KW;
+    t_kx = ALOAD == ALOAD_CONV2X2 ? tap & 1 : tap - t_ky * p.KW;
+  }
+  auto a_src = [&](const ARow& r, int k0, int chunk) -> const float* {
+    if (ALOAD == ALOAD_DENSE || !tap_walk) return a_ptr<ALOAD>(p, r, k0 + chunk);
+    if (ALOAD == ALOAD_CONV2X2) return p.A + r.base + ((int64_t)t_ky * p.Wd + t_kx) * p.Cin + t_c + chunk;
+    const int iy = r.iy0 + t_ky, ix = r.ix0 + t_kx;
+    if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero4;
+    return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cin + t_c + chunk;
+  };
   auto stage = [&](int kt, int buf) {
     if (ABL & 1) return;
     float* base = smem + buf * G::TILE_FLOATS;
     const int k0 = (kt_begin + kt) * BK;
 #pragma unroll
     for (int i = 0; i < G::A_DMA; ++i)
-      dma16(a_ptr<ALOAD>(p, arow[i], k0 + achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+      dma16(a_src(arow[i], k0, achunk[i]), base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+    if (ALOAD != ALOAD_DENSE && tap_walk) {
+      t_c += BK;
+      if (t_c == p.Cin) {
+        t_c = 0;
+        if (++t_kx == (ALOAD == ALOAD_CONV2X2 ? 2 : p.KW)) t_kx = 0, ++t_ky;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < G::B_DMA; ++i)
       dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
