@@ -28,64 +28,77 @@
 
 namespace {
 
-template <int C, int HC, int NW, int PX = 1>
+template <int C, int HC, int NW, int PX = 1, int HS = 1>
 struct MlpGeo {
   static constexpr int NT = 64 * NW;
   static constexpr int PXW = 16 * PX;                                      // pixels per wave
   static constexpr int W1F = HC * C, W2F = C * HC, CHUNK_F = W1F + W2F;   // floats per chunk
   static constexpr int NCH = 4 * C / HC;                                   // hidden chunks
+  static constexpr int NCHH = NCH / HS;                                    // chunks per hidden part
+  static constexpr int STAGE_F = HS * CHUNK_F;                             // one chunk per part
   static constexpr int W1_PIECES = W1F / 256, PIECES = CHUNK_F / 256;      // 1-KiB LDS-DMA pieces
-  static constexpr int PPW = PIECES / NW;                                  // pieces per wave
+  static constexpr int PPW = HS * PIECES / NW;                             // pieces per wave
+  static_assert(NCH % HS == 0 && NW % HS == 0 && (HS * PIECES) % NW == 0, "HS");
   static constexpr int RC1 = C / 4, RC2 = HC / 4;                          // 16-B chunks per row
   static_assert(C % 32 == 0 && RC1 % 8 == 0, "C");
   static_assert(HC == 16 || HC == 32, "HC");
-  static_assert(PIECES % NW == 0 && W1F % 256 == 0 && W2F % 256 == 0, "pieces");
+  static_assert(W1F % 256 == 0 && W2F % 256 == 0, "pieces");
   // chunk swizzles (XOR inside aligned groups of 16 / 8 / 4 chunks): conflict-free for the
   // fragment reads (row = 16 blk + (l & 15), chunk = 4 g + (l >> 4)), checked exhaustively
   static PIPNET_DEV int f1(int r) { return RC1 % 16 == 0 ? (r & 15) : (r & 7); }
   static PIPNET_DEV int f2(int r) { return HC == 32 ? (r & 7) : ((r >> 1) & 3); }
 };
 
-// PX = 16-pixel groups per wave: each W fragment read from LDS feeds PX MFMAs.
-template <int C, int HC, int NW, int PX>
+// PX = 16-pixel groups per wave: each W fragment read from LDS feeds PX MFMAs.  HS = hidden
+// parts: HS waves share a pixel group, wave part j contracting hidden chunks [j NCH/HS, (j+1)
+// NCH/HS) (both parts' chunks staged side by side), the partial out^T summed part 0 + part 1
+// through LDS before the epilogue -- HS x the waves per pixel (C5's stage 2 has 1024 pixel
+// groups: one wave per SIMD at HS = 1).  The hidden order, and so the rounding, depends on HS
+// only (never on M), so a fixed HS per C keeps the results batch-invariant.  The product uses
+// HS = 1 for both C (HS = 2 helps C5's stage 2 but not C2's, profiles/r02/mlp_lab.txt).
+template <int C, int HC, int NW, int PX, int HS = 1>
 __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
                                                               const float* __restrict__ W2,
                                                               const float* __restrict__ b2,
                                                               const float* __restrict__ gamma, float* x, int M) {
-  using G = MlpGeo<C, HC, NW, PX>;
-  // one LDS array (a second __shared__ object can make hipcc drain the DMA early): two chunk
-  // buffers, then b1 (staged once: a per-chunk global load of it would wait for the DMA)
-  __shared__ __attribute__((aligned(16))) float smem[2 * G::CHUNK_F + 4 * C];
-  float* sb1 = smem + 2 * G::CHUNK_F;
+  using G = MlpGeo<C, HC, NW, PX, HS>;
+  // one LDS array (a second __shared__ object can make hipcc drain the DMA early): two stage
+  // buffers (HS chunks each), then b1 (staged once: a per-chunk global load of it would wait
+  // for the DMA)
+  __shared__ __attribute__((aligned(16))) float smem[2 * G::STAGE_F + 4 * C];
+  float* sb1 = smem + 2 * G::STAGE_F;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int part = wid % HS, grp = wid / HS;
   const int q = lane >> 4, pl = lane & 15;
-  const int pix0 = blockIdx.x * (G::PXW * NW) + G::PXW * wid + pl;   // pixel of group 0; group u: + 16 u
+  const int pix0 = blockIdx.x * (G::PXW * NW / HS) + G::PXW * grp + pl;   // pixel of group 0; group u: + 16 u
 
-  // ---- LDS-DMA sources of this wave's pieces (chunk 0); chunk c adds c*HC*C (W1) / c*HC (W2) ----
+  // ---- LDS-DMA sources of this wave's pieces (stage 0); piece P of a stage belongs to part
+  // P / PIECES, whose chunk i is chunk part*NCHH + i: it adds that chunk's c*HC*C (W1) / c*HC (W2) ----
   const float* src[G::PPW];
   int dst[G::PPW];
   bool is_w1[G::PPW];
 #pragma unroll
   for (int j = 0; j < G::PPW; ++j) {
-    const int p = wid + NW * j;
-    dst[j] = p * 256;
+    const int pp = wid + NW * j;
+    const int pt = pp / G::PIECES, p = pp - pt * G::PIECES;
+    dst[j] = pt * G::CHUNK_F + p * 256;
     if (p < G::W1_PIECES) {
       const int e = p * 64 + lane;                        // 16-B chunk index inside the W1 image
       const int r = e / G::RC1, pc = e - r * G::RC1;
-      src[j] = W1 + (int64_t)r * C + 4 * (pc ^ G::f1(r));
+      src[j] = W1 + (int64_t)r * C + 4 * (pc ^ G::f1(r)) + (int64_t)pt * G::NCHH * HC * C;
       is_w1[j] = true;
     } else {
       const int e = (p - G::W1_PIECES) * 64 + lane;
       const int r = e / G::RC2, pc = e - r * G::RC2;
-      src[j] = W2 + (int64_t)r * (4 * C) + 4 * (pc ^ G::f2(r));
+      src[j] = W2 + (int64_t)r * (4 * C) + 4 * (pc ^ G::f2(r)) + (int64_t)pt * G::NCHH * HC;
       is_w1[j] = false;
     }
   }
-  auto stage = [&](int ch) {
-    float* base = smem + (ch & 1) * G::CHUNK_F;
+  auto stage = [&](int ch) {                           // ch = chunk index within a part
+    float* base = smem + (ch & 1) * G::STAGE_F;
 #pragma unroll
     for (int j = 0; j < G::PPW; ++j) {
       const float* s = src[j] + (is_w1[j] ? (int64_t)ch * HC * C : (int64_t)ch * HC);
@@ -122,11 +135,12 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   };
   constexpr int NHB = HC / 16;
 
-  for (int ch = 0; ch < G::NCH; ++ch) {
-    // this wave's pieces of chunk ch landed, every wave's reads of chunk ch-1 retired
+  for (int ci = 0; ci < G::NCHH; ++ci) {
+    // this wave's pieces of stage ci landed, every wave's reads of stage ci-1 retired
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (ch + 1 < G::NCH) stage(ch + 1);                 // into the buffer of chunk ch-1
-    const float* buf = smem + (ch & 1) * G::CHUNK_F;
+    if (ci + 1 < G::NCHH) stage(ci + 1);                // into the buffer of stage ci-1
+    const float* buf = smem + (ci & 1) * G::STAGE_F + part * G::CHUNK_F;
+    const int ch = part * G::NCHH + ci;                 // global hidden chunk
     // GEMM1: h^T[16 hb + 4q + i][pixel] for the NHB hidden blocks of the chunk; consecutive
     // MFMAs go to different accumulators (16x16x4: 40-cycle dependent latency, 32-cycle issue)
     f32x4 h[PX][NHB];
@@ -174,6 +188,26 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
             acc[u][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cb][s], h[u][hb][s], acc[u][cb], 0, 0, 0);
     }
   }
+  if constexpr (HS > 1) {
+    // part sums through LDS (the stage buffers are free once every wave passed this barrier):
+    // parts 1.. store, part 0 adds them in part order
+    static_assert(HS == 2, "HS");
+    static_assert((NW / HS) * 64 * PX * C / 4 <= 2 * G::STAGE_F, "part-sum LDS");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float* ex = smem + (grp * 64 + lane) * (PX * C / 4);
+    if (part == 1) {
+#pragma unroll
+      for (int u = 0; u < PX; ++u)
+#pragma unroll
+        for (int cb = 0; cb < C / 16; ++cb) st4(ex + (u * (C / 16) + cb) * 4, acc[u][cb]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (part != 0) return;
+#pragma unroll
+    for (int u = 0; u < PX; ++u)
+#pragma unroll
+      for (int cb = 0; cb < C / 16; ++cb) acc[u][cb] = acc[u][cb] + ld4(ex + (u * (C / 16) + cb) * 4);
+  }
   // ---- epilogue: x[pixel][c .. c+3] += gamma * (acc + b2), c = 16 cb + 4 q ----
 #pragma unroll
   for (int u = 0; u < PX; ++u) {
@@ -191,12 +225,12 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   }
 }
 
-template <int C, int HC, int NW, int PX>
+template <int C, int HC, int NW, int PX, int HS = 1>
 int launch_mlp(const float* t, const float* W1, const float* b1, const float* W2, const float* b2, const float* gamma,
                float* x, int M, hipStream_t s) {
-  const int px = 16 * PX * NW;
-  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1, b1,
-                     W2, b2, gamma, x, M);
+  const int px = 16 * PX * NW / HS;
+  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX, HS>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1,
+                     b1, W2, b2, gamma, x, M);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

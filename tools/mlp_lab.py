@@ -18,7 +18,7 @@ from count_pipnet_amd import build  # noqa: E402
 from count_pipnet_amd import kernels as K  # noqa: E402
 
 SO = os.path.join(HERE, "libmlp_lab.so")
-VARIANTS = {96: [0, 1, 2, 4, 5], 192: [0, 11, 12, 13, 14]}
+VARIANTS = {96: [0, 31, 32, 33], 192: [0, 13, 12, 21, 24, 25]}
 
 
 def main():
