@@ -333,11 +333,11 @@ def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20) -> str:
     """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_f32)."""
     if c == 96:
         nw = 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
-        return f"cnblock_mlp_kernel<96, 32, {nw}, 1>"
+        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
     if m >= 32768:
-        return "cnblock_mlp_kernel<192, 16, 8, 1>"
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 1>"
     nw = 4 if m >= 8192 else 2 if m >= 4096 else 1
-    return f"cnblock_mlp_kernel<192, 32, {nw}, 1>"
+    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
 
 
 def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor) -> Tensor:
