@@ -269,6 +269,15 @@ PIPNET_DEV float exp1_from_bits(uint32_t w) {
   return -logf(u);
 }
 
+// log E for E = -log u of the same 24-bit uniform, on the hardware log2 (v_log_f32, ~1 ulp):
+// ln E = ln2 * log2(-log2 u) + ln(ln2).  u in [2^-25, 1 - 2^-25] keeps both arguments normal.
+// For the hard Philox head only -- its noise is this library's own draw; the injected-noise and
+// soft paths keep the libm forms they share with the oracle.
+PIPNET_DEV float log_exp1_from_bits_fast(uint32_t w) {
+  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  return fmaf(__builtin_amdgcn_logf(-__builtin_amdgcn_logf(u)), 0.69314718f, -0.36651292f);
+}
+
 // One wave per pixel, four consecutive channels per lane (float4 logits / proto): the noise
 // of channels 4k..4k+3 of pixel (b, pix) is the Philox block (offset + (b*HW + pix)*P/4 + k)
 // -- one block per four elements, no word wasted.  Per pixel: z = (x - log E) / tau, argmax
@@ -292,6 +301,9 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
                                                                     int32_t* __restrict__ hist,
                                                                     float* __restrict__ sums = nullptr) {
   constexpr int NJ4 = (NJ + 3) / 4;         // float4 channel chunks per lane (256 channels each)
+  // hard head on Philox noise: hardware log2 / exp2 (~1 ulp) for the noise and the running
+  // sum -- 3 transcendentals per element dominated its VALU time at C5
+  constexpr bool FAST = !SOFT && !NOISE;
   if (seed_dev) seed = *seed_dev;            // graph-replay form: the seed lives in device memory
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
@@ -333,25 +345,26 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
     for (int j = 0; j < NJ4; ++j) {
       const int c = 4 * lane + 256 * j;
       if (c < P) {
-        float E[4];
+        float lE[4];                                       // log of the Exp(1) draw
         if constexpr (NOISE) {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) E[e] = exp_noise[((int64_t)b * P + c + e) * HW + pix];   // NCHW draw
+          for (int e = 0; e < 4; ++e) lE[e] = logf(exp_noise[((int64_t)b * P + c + e) * HW + pix]);   // NCHW draw
         } else {
           uint32_t w[4];
           philox4(seed, offset + (uint64_t)((base + c) >> 2), w);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) E[e] = exp1_from_bits(w[e]);
+          for (int e = 0; e < 4; ++e) lE[e] = FAST ? log_exp1_from_bits_fast(w[e]) : logf(exp1_from_bits(w[e]));
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float zv = (xc[j][e] - logf(E[e])) * inv_tau;
+          const float zv = (xc[j][e] - lE[e]) * inv_tau;
           if constexpr (SOFT) {
             z[j][e] = zv;
             if (zv > m) { m = zv; mi = c + e; }
           } else {
             const bool up = zv > m;
-            const float d = expf(up ? m - zv : zv - m);      // exp(-|zv - m|); exp(-inf) = 0 first
+            const float nd = up ? m - zv : zv - m;             // -|zv - m|; -inf first
+            const float d = FAST ? __builtin_amdgcn_exp2f(nd * 1.44269504f) : expf(nd);
             ls = up ? fmaf(ls, d, 1.0f) : ls + d;
             if (up) { m = zv; mi = c + e; }
           }

@@ -182,6 +182,23 @@ def test_count_gumbel_philox_statistics(gpu):
     assert not torch.equal(hist, hist3)
 
 
+def test_count_gumbel_philox_follows_softmax(gpu):
+    """Gumbel-max law of the in-kernel noise (hardware log2 / exp2 path): the argmax of
+    (x - log E) / tau falls on channel i with probability softmax(x)_i, for any tau."""
+    p, hw, b = 8, 8192, 4
+    x = torch.linspace(-1.5, 1.0, p)
+    logits = x.view(1, 1, 1, p).expand(b, hw, 1, p).contiguous().to(gpu)
+    probs = torch.softmax(x.double(), 0)
+    for tau, seed in ((1.0, 7), (0.5, 8)):
+        proto, hist = K.count_gumbel(logits, tau, None, seed=seed)
+        h = hist.cpu().double().sum(0)
+        expected = probs * b * hw
+        chi2 = float(((h - expected) ** 2 / expected).sum())
+        assert chi2 < 40.0, (tau, chi2)       # 7 dof: p(chi2 > 40) ~ 1e-6
+        s = proto.sum(dim=3)
+        assert torch.allclose(s, torch.ones_like(s)) and torch.equal((proto > 0).sum(dim=3), torch.ones_like(s).long())
+
+
 def test_count_finish_and_encode(gpu):
     hist = torch.tensor([[0, 1, 2, 3, 4, 7]], dtype=torch.int32, device=gpu)
     raw, cl = K.count_finish(hist, None, 3, True)

@@ -28,6 +28,7 @@ def shapes(batch=64):
         m = batch * hw * hw
         out.append((f"s{d}_fc1", m, 4 * d, d, _lib.EPI_BIAS_GELU))
         out.append((f"s{d}_fc2", m, d, 4 * d, _lib.EPI_RESID))
+    out.append(("c5_addon", 64 * 16 * 16, 2048, 192, _lib.EPI_BIAS))    # C5: 1x1 add-on 192 -> 2048
     return out
 
 
