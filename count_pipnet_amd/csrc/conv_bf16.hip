@@ -52,11 +52,41 @@ bool is_s3_epi(int epi) {
   return epi == PIPNET_EPI_S3_GELU || epi == PIPNET_EPI_F32_BIAS || epi == PIPNET_EPI_F32_RESID;
 }
 
+// 3x3 / stride 1 / pad 1 convs whose halo fits the kernel's 384 LDS rows (256 + 2W + 2):
+// the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer choice, never M.
+bool halo_ok(const ConvParams& p, int epi) {
+  return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
+         p.seg == 0 && p.Cin % 32 == 0 && p.Wd <= 63 && p.N >= 256 && !is_s3_epi(epi);
+}
+
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
-  if (v < 0) v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
-  if (v > 7 || ((v == 5 || v == 7) && !pp_ok)) return PIPNET_ERR_ARG;
+  const bool hk = ALOAD == ALOAD_CONV && halo_ok(p, epi);
+  if (v < 0) {
+    v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
+    if (v == 5 && hk) v = 8;
+  }
+  if (v > 8 || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk)) return PIPNET_ERR_ARG;
+  if (v == 8) {                                  // 256 x 256 ping-pong with the LDS input halo
+    p.nt = (p.N + 255) / 256;
+    p.mt = (p.M + 255) / 256;
+    p.group_m = choose_group_m(p.K);
+    const dim3 grid(p.mt * p.nt);
+    switch (epi) {
+      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS_RELU:
+        hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_BIAS_RESID_RELU:
+        hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(512), 0, s, p);
+        break;
+      default: return PIPNET_ERR_ARG;
+    }
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   if (v == 7) {                                  // 256 x 192 ping-pong (split epilogues only)
     p.nt = (p.N + 191) / 192;
     p.mt = (p.M + 255) / 256;

@@ -68,7 +68,7 @@ def test_conv2d_nhwc_bf16(gpu, cin, cout, h, k, s, pad, epi):
     _close_bf16(out.cpu(), ref)
 
 
-@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("tile", [0, 1, 2, 3, 4, 5, 6, 8])
 @pytest.mark.parametrize("cin,cout,h,k,s,pad,epi", [
     (64, 256, 19, 3, 1, 1, _lib.EPI_BIAS_RESID_RELU),   # M = 1083: ragged in every tile size
     (256, 520, 10, 1, 2, 0, _lib.EPI_BIAS),             # N = 520: ragged N tile, strided 1x1
@@ -81,6 +81,8 @@ def test_conv2d_nhwc_bf16_every_tile(gpu, tile, cin, cout, h, k, s, pad, epi):
     """Each workgroup tile (64x128, 128x128, 256x256, ping-pong 256x256, 256x64) forced on ragged shapes."""
     if tile == 5 and not ((k == 1 and s == 1 and pad == 0) or cin % 32 == 0):
         pytest.skip("the ping-pong tile needs whole-tap K tiles (Cin % 32 == 0)")
+    if tile == 8 and not (k == 3 and s == 1 and pad == 1 and cin % 32 == 0 and cout >= 256):
+        pytest.skip("the halo tile serves 3x3 stride-1 pad-1 convs with Cin % 32 == 0, N >= 256")
     g = torch.Generator().manual_seed(tile * 11 + cout)
     x = _bf(torch.randn(3, cin, h, h, generator=g))
     w = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
@@ -97,6 +99,51 @@ def test_conv2d_nhwc_bf16_every_tile(gpu, tile, cin, cout, h, k, s, pad, epi):
                              b.float().to(gpu), s, pad, epi, nhwc(r) if epi == _lib.EPI_BIAS_RESID_RELU else None,
                              tile=tile)
     _close_bf16(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("b,cin,cout,h,w,epi", [
+    (3, 64, 256, 7, 9, _lib.EPI_BIAS_RESID_RELU),   # non-square, several images per 256-pixel tile
+    (2, 96, 264, 5, 1, _lib.EPI_BIAS_RELU),         # W = 1 (every kx != 1 tap is padding), ragged N
+    (1, 32, 256, 63, 63, _lib.EPI_BIAS),            # widest halo (256 + 2*63 + 2 = 384 rows), K 288 -> 320
+    (5, 256, 256, 28, 28, _lib.EPI_BIAS_RELU),      # layer3 conv2 at 28^2 (C3), ragged last tile
+    (2, 512, 512, 28, 13, _lib.EPI_NONE),           # layer4 conv2 channels: 16 chunks x 9 taps
+])
+def test_conv_bf16_halo(gpu, b, cin, cout, h, w, epi):
+    """3x3 stride-1 convolutions on the LDS-halo ping-pong tile (automatic choice, tile 8):
+    K walked chunk-major / tap-minor, taps across row and image boundaries of the linear
+    pixel index read the zero block.  Same one-ulp bar as every other tile, and the
+    automatic choice must be the halo kernel."""
+    g = torch.Generator().manual_seed(b * 7 + cin + cout + h * 3 + w)
+    x = _bf(torch.randn(b, cin, h, w, generator=g))
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / (cin * 9) ** 0.5
+    bias = torch.randn(cout, generator=g).double()
+    y = F.conv2d(x, _bf(wt), bias if epi != _lib.EPI_NONE else None, stride=1, padding=1)
+    r = _bf(torch.randn(*y.shape, generator=g))
+    if epi == _lib.EPI_BIAS_RELU:
+        y = torch.relu(y)
+    if epi == _lib.EPI_BIAS_RESID_RELU:
+        y = torch.relu(y + r)
+    ref = _bf(y.float()).permute(0, 2, 3, 1)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu)  # noqa: E731
+    wp = K.pack_conv_weight_bf16(wt.permute(0, 2, 3, 1).contiguous().to(gpu))
+    assert K.bf16_conv_tile(b * h * w, cout, halo_ok=True) == 8
+    outs = [K.conv2d_nhwc_bf16(nhwc(x), wp, 3, 3, bias.float().to(gpu) if epi != _lib.EPI_NONE else None, 1, 1, epi,
+                               nhwc(r) if epi == _lib.EPI_BIAS_RESID_RELU else None, tile=t) for t in (-1, 8)]
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    _close_bf16(outs[0].cpu(), ref)
+
+
+def test_conv_bf16_halo_batch_invariant(gpu):
+    """The halo kernel's per-pixel arithmetic does not depend on the batch a pixel is in."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(6, 28, 28, 256, generator=g).to(torch.bfloat16).to(gpu)
+    wp = K.pack_conv_weight_bf16((torch.randn(256, 3, 3, 256, generator=g) / 48.0).to(gpu))
+    bias = torch.randn(256, generator=g).to(gpu)
+    full = K.conv2d_nhwc_bf16(x, wp, 3, 3, bias, 1, 1, _lib.EPI_BIAS_RELU)
+    part = K.conv2d_nhwc_bf16(x[2:5].contiguous(), wp, 3, 3, bias, 1, 1, _lib.EPI_BIAS_RELU)
+    torch.cuda.synchronize()
+    assert torch.equal(full[2:5], part)
 
 
 def test_conv_bf16_layout_asymmetric(gpu):
