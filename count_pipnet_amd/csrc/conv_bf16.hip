@@ -52,11 +52,11 @@ bool is_s3_epi(int epi) {
   return epi == PIPNET_EPI_S3_GELU || epi == PIPNET_EPI_F32_BIAS || epi == PIPNET_EPI_F32_RESID;
 }
 
-// 3x3 / stride 1 / pad 1 convs whose halo fits the kernel's 384 LDS rows (256 + 2W + 2):
+// 3x3 / stride 1 / pad 1 convs whose halo fits the kernel's 320 LDS rows (256 + 2W + 2):
 // the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer choice, never M.
 bool halo_ok(const ConvParams& p, int epi) {
   return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
-         p.seg == 0 && p.Cin % 32 == 0 && p.Wd <= 63 && p.N >= 256 && !is_s3_epi(epi);
+         p.seg == 0 && p.Cin % 64 == 0 && p.Wd <= 31 && p.N >= 256 && !is_s3_epi(epi);
 }
 
 template <int ALOAD>

@@ -728,62 +728,46 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 // LDS port -- is what holds the big layers at 35-40 % of the bf16 peak (profiles/r02/
 // bf16_lab.txt: the B-only-DMA ablation recovers most of the no-DMA rate).  For a 3x3
 // stride-1 conv the nine taps of a 256-pixel tile read the same input pixels shifted by
-// (ky-1)*W + (kx-1) in the linear NHWC pixel index.  This kernel walks K as (channel chunk
-// c of 32, tap t) instead of (tap, channel): per chunk it stages the pixel range
-// [m0 - W - 1, m0 + 256 + W + 1) once (the "halo", 256 + 2W + 2 rows of 64 B, <= 384 rows),
-// and the nine K-tiles of the chunk read their A fragments from it at row offset
-// ky*W + kx; only B still streams per K-tile.  A bytes per K-tile fall from 16 KiB to
-// 24 KiB / 9 (W <= 63).  Taps that fall outside the image (padding, or a row / image
-// boundary the linear index would wrap across) read a 256-B zero block at the same bank slot.
+// (ky-1)*W + (kx-1) in the linear NHWC pixel index.  This kernel stages, per pair of 32-channel
+// chunks, the pixel range [m0 - W - 1, m0 + 256 + W + 1) once (the "halo": 256 + 2W + 2 <= 320
+// rows of 64 B per chunk), and the 18 K-tiles of the pair -- taps t = 0..8, each for chunk
+// halves h = 0, 1 -- read their A fragments from it at row offset ky*W + kx; only B still
+// streams per K-tile.  K order (pair, tap, half): consecutive K-tiles read the two 64-B halves
+// of the same 128-B weight line, as the pp kernel's (tap, chunk) order does (a (chunk, tap)
+// order that revisits each line 9 K-tiles later measured 15-20 % slower than pp).  A bytes per
+// K-tile fall from 16 KiB to 40 KiB / 18.  Taps that fall outside the image (padding, or a row
+// / image boundary the linear index would wrap across) read a 256-B zero block at the same
+// bank slot.
 //
 // Halo rows: chunk q of row r at physical chunk q ^ hs(r), hs(r) = ((r >> 2) & 1) << 1 --
 // conflict-free for the 16x16x32 operand map at ANY row offset (each ds_read_b128 lane group
 // of 16 reads 16 consecutive rows; checked for all offsets: every group hits 16 distinct
 // 16-B bank slots), unlike the pp swizzle, which is conflict-free only on 16-row-aligned
-// blocks.  Pipeline, barriers, wave groups and epilogue are those of conv_bf16_pp_kernel:
-// B of K-tile kt+DB is fetched in phase 0 of K-tile kt; the halo of chunk c+1 (3 x 1 KiB
-// pieces per wave) in phase 1 of the chunk's tap 1 (its buffer was last read two K-tiles
-// earlier, by chunk c-1), so it is always older than the B pieces the counted waits retire.
-// The accumulation order (chunk-major, tap-minor) depends on the layer only, never on M.
-// Requirements: KH = KW = 3, stride 1, pad 1, Cin % 32 == 0, K == 9 Cin, W <= 63, no seg.
+// blocks.  A lane's 8 fragment rows differ by multiples of 16, so for a given tap the
+// swizzle term is one per lane and the 8 fragment addresses differ by immediates.
+// Pipeline, barriers, wave groups and epilogue are those of conv_bf16_pp_kernel: B of K-tile
+// kt+2 is fetched in phase 0 of K-tile kt; the halo of pair P+1 (5 x 1 KiB pieces per wave)
+// in phase 1 of K-tile 18P + 1 (its two slots were last read two K-tiles earlier, by pair
+// P-1), so it is always older than the B pieces the counted waits retire.  The accumulation
+// order depends on the layer only, never on M.
+// Requirements: KH = KW = 3, stride 1, pad 1, Cin % 64 == 0, W <= 31, no seg.
 // ======================================================================================
 namespace ph {
+constexpr int DB = 2, NS = DB + 2;
 constexpr int BSTAGE = pp::BN * pp::ROWB;             // 16 KiB: the B rows of one K-tile
-constexpr int HALO_ROWS = 384;                        // 24 DMA pieces of 16 rows
-constexpr int HALO_BYTES = HALO_ROWS * pp::ROWB;      // 24 KiB
-template <int DB>
-constexpr int off_halo() { return (DB + 2) * BSTAGE; }
-template <int DB>
-constexpr int off_zero() { return off_halo<DB>() + 2 * HALO_BYTES; }
-template <int DB>
-constexpr int smem_bytes() { return off_zero<DB>() + 256 > pp::EPI_BYTES ? off_zero<DB>() + 256 : pp::EPI_BYTES; }
+constexpr int HALO_ROWS = 320;                        // 20 DMA pieces of 16 rows per chunk
+constexpr int HALO_BYTES = HALO_ROWS * pp::ROWB;      // 20 KiB
+constexpr int OFF_HALO = NS * BSTAGE;                 // 4 halo slots: pair parity x chunk half
+constexpr int OFF_ZERO = OFF_HALO + 4 * HALO_BYTES;
+constexpr int SMEM = OFF_ZERO + 256 > pp::EPI_BYTES ? OFF_ZERO + 256 : pp::EPI_BYTES;
 PIPNET_DEV int hs(int r) { return ((r >> 2) & 1) << 1; }
 }  // namespace ph
 
-PIPNET_DEV void pp_wait_vm_any(int n) {
-  switch (n) {
-    case 0: pp_wait_vm<0>(); break;
-    case 1: pp_wait_vm<1>(); break;
-    case 2: pp_wait_vm<2>(); break;
-    case 3: pp_wait_vm<3>(); break;
-    case 4: pp_wait_vm<4>(); break;
-    case 5: pp_wait_vm<5>(); break;
-    case 6: pp_wait_vm<6>(); break;
-    case 7: pp_wait_vm<7>(); break;
-    case 8: pp_wait_vm<8>(); break;
-    case 9: pp_wait_vm<9>(); break;
-    case 10: pp_wait_vm<10>(); break;
-    case 11: pp_wait_vm<11>(); break;
-    default: pp_wait_vm<0>(); break;
-  }
-}
-
-template <int EPI, int DB = 2>
+template <int EPI>
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
   using namespace pp;
-  constexpr int NS = DB + 2;
-  static_assert(DB >= 2 && DB <= 3, "DB");
-  __shared__ __attribute__((aligned(256))) unsigned char smem[ph::smem_bytes<DB>()];
+  using ph::NS;
+  __shared__ __attribute__((aligned(256))) unsigned char smem[ph::SMEM];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
@@ -791,8 +775,8 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   int m0, n0;
   tile_coords(p, BM, BN, m0, n0);
   const int W = p.Wd, HW = p.H * p.Wd;
-  const int nch = p.Cin / BK;                                  // channel chunks
-  const int nk = 9 * nch;
+  const int npair = p.Cin / (2 * BK);
+  const int nk = 18 * npair;
 
   // ---- B DMA sources: pieces wid and wid + 8 (16 rows x 64 B each), pp swizzle ----
   const int drow = lane >> 2;
@@ -802,13 +786,17 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
     const int row = 16 * (wid + 8 * i) + drow;
     wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * ((lane & 3) ^ g(drow));
   }
-  // ---- halo DMA sources: pieces wid, wid + 8, wid + 16; halo row i = pixel m0 - W - 1 + i ----
-  int64_t hsrc[3];
+  // ---- halo DMA: 40 pieces per pair (20 per chunk half), 5 per wave: piece e = wid + 8 i is
+  // chunk half e / 20, halo rows 16 (e % 20) + ...; halo row i = pixel m0 - W - 1 + i ----
+  int64_t hsrc[5];
+  int hdst[5];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int row = 16 * (wid + 8 * i) + drow;
+  for (int i = 0; i < 5; ++i) {
+    const int e = wid + 8 * i, h = e >= 20 ? 1 : 0, pc = e - 20 * h;
+    const int row = 16 * pc + drow;
     const int pix = min(max(m0 - W - 1 + row, 0), p.M - 1);
-    hsrc[i] = (int64_t)pix * p.Cin + 8 * ((lane & 3) ^ ph::hs(row));
+    hsrc[i] = (int64_t)pix * p.Cin + h * BK + 8 * ((lane & 3) ^ ph::hs(row));
+    hdst[i] = h * ph::HALO_BYTES + pc * 1024;
   }
   // ---- this lane's 8 fragment rows: tile row wr*128 + j*16 + (lane & 15); 9-bit tap masks ----
   const int fr = lane & 15;
@@ -829,11 +817,11 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
     }
     vmask[j] = mk;
   }
-  if (tid < 16) *reinterpret_cast<u32x4*>(smem + ph::off_zero<DB>() + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
+  if (tid < 16) *reinterpret_cast<u32x4*>(smem + ph::OFF_ZERO + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 
   auto stage_b = [&](int kt) {
-    const int c = kt / 9, t = kt - 9 * c;
-    const int k0 = t * p.Cin + c * BK;
+    const int P = kt / 18, rem = kt - 18 * P;
+    const int k0 = (rem >> 1) * p.Cin + (2 * P + (rem & 1)) * BK;
     unsigned char* base = smem + (kt % NS) * ph::BSTAGE;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -841,13 +829,12 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
                                        (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
                                        0, 0);
   };
-  auto stage_halo = [&](int c) {
-    unsigned char* base = smem + ph::off_halo<DB>() + (c & 1) * ph::HALO_BYTES;
+  auto stage_halo = [&](int P) {
+    unsigned char* base = smem + ph::OFF_HALO + (P & 1) * 2 * ph::HALO_BYTES;
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + hsrc[i] + c * BK),
-                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
-                                       0, 0);
+    for (int i = 0; i < 5; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + hsrc[i] + P * 2 * BK),
+                                       (__attribute__((address_space(3))) void*)(base + hdst[i]), 16, 0, 0);
   };
   const int fofs_b = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
   const int q16 = (lane >> 4) << 4;
@@ -855,14 +842,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
 #pragma unroll
     for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const bf16x8v*>(st + (wc * 64 + n * 16) * ROWB + fofs_b);
   };
-  const unsigned char* zb = smem + ph::off_zero<DB>();
-  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* hb, int half, int toff, int t) {
+  const unsigned char* zb = smem + ph::OFF_ZERO;
+  // lane byte offset inside a halo slot for this tap (fragment rows j add j * 1 KiB)
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* hb, int half, int loff, unsigned tbit) {
+    const unsigned char* zl = zb + (loff & 255);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = half * 4 + r;
-      const int hr = wr * 128 + j * 16 + fr + toff;
-      const int off = hr * ROWB + (q16 ^ ((hr << 3) & 32));    // chunk ^ hs(hr), in bytes
-      const unsigned char* ptr = ((vmask[j] >> t) & 1u) ? hb + off : zb + (off & 255);
+      const unsigned char* ptr = (vmask[j] & tbit) ? hb + loff + j * 1024 : zl;
       fa[r] = *reinterpret_cast<const bf16x8v*>(ptr);
     }
   };
@@ -873,62 +860,66 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  // halo of chunk c+1 is issued in phase 1 of K-tile 9c + 1
-  auto halo_at = [&](int kt) { return kt >= 0 && kt % 9 == 1 && kt / 9 + 1 < nch; };
-  // pieces issued after B(kt+1) (phase 0 of K-tile kt+1-DB) by the wait in phase 1 of K-tile kt
-  auto younger_than_b = [&](int kt) {
-    int n = 0;
-#pragma unroll
-    for (int j = 2; j <= DB; ++j) n += (kt + j < nk) ? 2 : 0;
-#pragma unroll
-    for (int d = 0; d < DB; ++d) n += halo_at(kt - d) ? 3 : 0;
-    return n;
-  };
-  // prologue: halo(0), B(0) .. B(DB-1); wait for halo(0) and B(0)
+  // prologue: halo(0), B(0), B(1); wait for halo(0) and B(0)
   stage_halo(0);
-#pragma unroll
-  for (int i = 0; i < DB; ++i)
-    if (i < nk) stage_b(i);
-  pp_wait_vm_any(2 * (min(DB, nk) - 1));
+  stage_b(0);
+  if (1 < nk) stage_b(1);
+  if (nk > 1) pp_wait_vm<2>();
+  else pp_wait_vm<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // zero block written
   pp_barrier();
   if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
 
+  // K-tile kt = 18 P + 2 t + h.  B of K-tile kt+2 is fetched in phase 0 of kt; the halo of
+  // pair P+1 in phase 1 of (t, h) = (0, 1).  The wait in phase 1 of kt retires B(kt+1): younger
+  // are B(kt+2) and the halo pieces issued at (0, 1) or, for (1, 0), one K-tile earlier; none
+  // in the last tap of the last pair.  Everything but the MFMA stream is scalar bookkeeping
+  // kept branch-light (one compile-time h per unrolled half).
   bf16x8v fa[4], fb[4];
-  int c = 0, t = 0, ky = 0, kx = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    const unsigned char* st = smem + (kt % NS) * ph::BSTAGE;
-    const unsigned char* hb = smem + ph::off_halo<DB>() + (c & 1) * ph::HALO_BYTES;
-    const int toff = ky * W + kx;
-    // ---- phase 0: rows 0..63 of the wave's block ----
-    if (kt + DB < nk) stage_b(kt + DB);
-    read_b(fb, st);
-    read_a(fa, hb, 0, toff, t);
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
+  const int lrow = wr * 128 + fr;
+  int kt = 0;
+  for (int P = 0; P < npair; ++P) {
+    const bool more = P + 1 < npair;
+    const unsigned char* hp = smem + ph::OFF_HALO + (P & 1) * 2 * ph::HALO_BYTES;
+    for (int t = 0; t < 9; ++t) {
+      const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
+      const int hr = lrow + ky * W + kx;                       // this lane's halo row of fragment j = 0
+      const int loff = hr * ROWB + (q16 ^ ((hr << 3) & 32));   // chunk ^ hs(hr), in bytes
+      const unsigned tbit = 1u << t;
+      const bool last = !more && t == 8;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+      for (int h = 0; h < 2; ++h, ++kt) {
+        const unsigned char* st = smem + (kt & (NS - 1)) * ph::BSTAGE;
+        const unsigned char* hb = hp + h * ph::HALO_BYTES;
+        // ---- phase 0: rows 0..63 of the wave's block ----
+        if (!last) stage_b(kt + 2);
+        read_b(fb, st);
+        read_a(fa, hb, 0, loff, tbit);
+        pp_barrier();
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    // ---- phase 1: rows 64..127; halo of the next chunk at tap 1; wait for K-tile kt+1 ----
-    if (halo_at(kt)) stage_halo(c + 1);
-    read_a(fa, hb, 1, toff, t);
-    pp_wait_vm_any(younger_than_b(kt));
-    pp_barrier();
-    __builtin_amdgcn_s_setprio(1);
+        for (int r = 0; r < 4; ++r)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+          for (int n = 0; n < 4; ++n)
+            acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+        // ---- phase 1: rows 64..127 ----
+        if (h == 1 && t == 0 && more) stage_halo(P + 1);
+        read_a(fa, hb, 1, loff, tbit);
+        if (last) pp_wait_vm<0>();
+        else if (more && ((h == 1 && t == 0) || (h == 0 && t == 1))) pp_wait_vm<7>();
+        else pp_wait_vm<2>();
+        pp_barrier();
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-        acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    pp_barrier();
-    ++t;
-    if (++kx == 3) {
-      kx = 0;
-      if (++ky == 3) ky = 0, t = 0, ++c;
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        pp_barrier();
+      }
     }
   }
   if (wr == 0) pp_barrier();                                   // re-align the groups

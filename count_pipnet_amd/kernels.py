@@ -197,7 +197,7 @@ def _chk_bf(t: Tensor, what: str) -> None:
 
 def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int = 0, halo_ok: bool = False) -> int:
     """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
-    8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 32 == 0, W <= 63),
+    8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31),
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
     MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
@@ -229,7 +229,7 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     """rocprof name of the bf16 conv instantiation."""
     t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok) if tile < 0 else tile
     if t == 8:
-        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, 2>"
+        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}>"
     if t == 5:
         return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4, 0, 2>"
     if t == 7:
@@ -271,7 +271,7 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
     pp_ok = (aload == 0 or cin % 32 == 0) and kp % 32 == 0
-    halo_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin % 32 == 0 and w <= 63 and cout >= 256
+    halo_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin % 64 == 0 and w <= 31 and cout >= 256
                and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, halo_ok=halo_ok), 2.0 * m * cout * k,
             lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
