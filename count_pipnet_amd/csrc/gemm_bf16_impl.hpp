@@ -495,16 +495,20 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
     s0 = *reinterpret_cast<const f32x4v*>(p.scale + n);
     s1 = *reinterpret_cast<const f32x4v*>(p.scale + n + 4);
   }
+  // residual rows of both halves requested up front: one HBM latency per tile, not two
+  bf16x8v rrs[2][8];
+  if (HAS_R) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    bf16x8v rr[8];
-    if (HAS_R) {
+    for (int half = 0; half < 2; ++half)
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
         const int m = min(m0 + wr * 128 + half * 64 + it * 8 + (lane >> 3), p.M - 1);
-        if (nok) rr[it] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
+        if (nok) rrs[half][it] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
       }
-    }
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    bf16x8v (&rr)[8] = rrs[half];
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -588,9 +592,11 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   // (tap, channel) of the K-tile the DMA fetches next, advanced incrementally (a 32-deep
   // K-tile never straddles a tap: Cin % 32 == 0), so no division in the loop.
   int d_c = 0, d_kx = 0, d_ky = 0;
+  // K-tiles past the valid K (K padded to 64) re-read the last valid one: the packed weights
+  // are zero there, so the products are exact zeros (finite activations) and no per-K-tile
+  // branch to a zero source is needed.
   auto a_src = [&](const ARow& r, int k0) -> const void* {
-    if (k0 >= p.Kv) return g_zero_bf;
-    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, k0) + dchunk;
+    if (ALOAD == ALOAD_DENSE) return p.A + r.base + seg_remap(p, min(k0, p.Kv - BK)) + dchunk;
     const int iy = r.iy0 + d_ky, ix = r.ix0 + d_kx;
     if ((unsigned)iy >= (unsigned)p.H || (unsigned)ix >= (unsigned)p.Wd) return g_zero_bf;
     return p.A + r.base + ((int64_t)iy * p.Wd + ix) * p.Cinp + seg_remap(p, d_c) + dchunk;
@@ -672,10 +678,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
     if constexpr ((ABL & 4) == 0) pp_barrier();
   };
   bf16x8v fa[4], fb[4];
-  for (int kt = 0; kt < nk; ++kt) {
+  // One K-tile.  STEADY (every K-tile but the last DB + 1): both DMA pieces exist and the wait
+  // count is the constant 4 (DB - 1) + 2 -- no per-K-tile count arithmetic or wait-count
+  // switch (that scalar bookkeeping and its branches lengthened every read segment).
+  auto ktile = [&](int kt, auto steady) {
+    constexpr bool STEADY = decltype(steady)::value;
     const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
     // ---- phase 0: rows 0..63 of the wave's block ----
-    if (kt + DB < nk) stage_b(kt + DB);                        // DMA before the reads (M0 write)
+    if (STEADY || kt + DB < nk) stage_b(kt + DB);              // DMA before the reads (M0 write)
     read_b(fb, st);
     read_a(fa, st, 0);
     bar();
@@ -688,10 +698,13 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
     bar();
     // ---- phase 1: rows 64..127; fetch A of K-tile kt+3 (DMA first: an M0 write for the DMA
     // would otherwise wait for this phase's fragment reads); wait for K-tile kt+1 ----
-    if (kt + DB + 1 < nk) stage_a(kt + DB + 1);
+    if (STEADY || kt + DB + 1 < nk) stage_a(kt + DB + 1);
     read_a(fa, st, 1);
     // wait for this wave's pieces of K-tile kt+1 (B(kt+1) is its last)
-    if constexpr ((ABL & 1) == 0) pp_wait_vm_dyn(younger_than_b(kt));
+    if constexpr ((ABL & 1) == 0) {
+      if constexpr (STEADY) pp_wait_vm<4 * (DB - 1) + 2>();
+      else pp_wait_vm_dyn(younger_than_b(kt));
+    }
     bar();
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -701,7 +714,10 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
         acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     bar();
-  }
+  };
+  int kt = 0;
+  for (; kt < nk - DB - 1; ++kt) ktile(kt, IntC<1>{});
+  for (; kt < nk; ++kt) ktile(kt, IntC<0>{});
   if (wr == 0) pp_barrier();                                   // re-align the groups
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pp_barrier();                                                // stage buffers free for the epilogue

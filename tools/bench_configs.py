@@ -74,7 +74,7 @@ def main():
     build.build()
     dev = torch.device("cuda:0")
     for name, cfg in CONFIGS.items():
-        if a.only and name != a.only:
+        if a.only and name not in a.only.split(","):
             continue
         net = make(cfg, dev)
         if a.stream_split:
