@@ -9,6 +9,20 @@ namespace {
 
 int grid_for(int64_t n) { return (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192); }
 
+// compute units of the current device (one persistent workgroup each), queried once
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
 int choose_group_m(int K) {
   const double panel = 128.0 * K * 2.0;
   int g = (int)(2.0 * 1024 * 1024 / panel);
@@ -63,11 +77,34 @@ template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
   const bool hk = ALOAD == ALOAD_CONV && halo_ok(p, epi);
+  // 1x1 convs with N % 256 == 0: the persistent ping-pong tile (9), same K order as tile 5
+  const bool pk = ALOAD == ALOAD_DENSE && pp_ok && p.N % 256 == 0 && !is_s3_epi(epi);
   if (v < 0) {
     v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
     if (v == 5 && hk) v = 8;
+    else if (v == 5 && pk) v = 9;
   }
-  if (v > 8 || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk)) return PIPNET_ERR_ARG;
+  if (v > 9 || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
+  if (v == 9) {                                  // persistent 256 x 256 ping-pong (1x1, N % 256 == 0)
+    p.nt = p.N / 256;
+    p.mt = (p.M + 255) / 256;
+    p.group_m = choose_group_m(p.K);
+    const int ntiles = p.mt * p.nt;
+    const dim3 grid(ntiles < num_cus() ? ntiles : num_cus());
+    switch (epi) {
+      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_NONE>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS>), grid, dim3(512), 0, s, p); break;
+      case PIPNET_EPI_BIAS_RELU:
+        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(512), 0, s, p);
+        break;
+      case PIPNET_EPI_BIAS_RESID_RELU:
+        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(512), 0, s, p);
+        break;
+      default: return PIPNET_ERR_ARG;
+    }
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   if (v == 8) {                                  // 256 x 256 ping-pong with the LDS input halo
     p.nt = (p.N + 255) / 256;
     p.mt = (p.M + 255) / 256;

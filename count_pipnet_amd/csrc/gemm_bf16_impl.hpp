@@ -737,6 +737,264 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 }
 
 // ======================================================================================
+// Persistent ping-pong tile for 1x1 (dense) convolutions with N % 256 == 0.
+//
+// One workgroup per CU walks tiles blockIdx.x, +gridDim.x, ... (the same XCD-grouped raster:
+// gridDim.x % 8 == 0 keeps a workgroup's tiles on its XCD's slice).  Between two tiles it
+// issues the next tile's first K-tiles (A0 B0 A1 B1 A2, the pp prologue) into the stage
+// buffers BEFORE the current tile's epilogue, and the epilogue re-lays the accumulators
+// through a separate 32 KiB region (per wave 16 rows x 64 fp32 at a time, XOR-swizzled rows:
+// physical column = c ^ (((r >> 2) & 3) << 4 | (r & 1) << 2), conflict-free for the MFMA-layout
+// writes and the 8-channel reads).  So the next tile's operand latency, the workgroup launch
+// and the store drain of the previous one overlap instead of idling the CU (the pp tile holds
+// 139 KiB of LDS: one workgroup per CU, nothing else covers those gaps; short-K layers such
+// as the bottleneck conv3 + residual spend a large share of each tile there).
+// Counting: every lane issues the same number of epilogue loads / stores (rows past M are
+// clamped to row M-1 -- they recompute row M-1's values from the clamped A row, so the
+// duplicate store writes identical bits; N % 256 == 0 so every column is valid), which keeps
+// the vmcnt waits exact: the next tile's K-tile 0 is retired with vmcnt(6 + stores), and
+// its first in-loop wait excludes the epilogue stores as well.
+// ======================================================================================
+namespace ppp {
+constexpr int OFF_EPI = 4 * pp::STAGE_BYTES;          // 128 KiB of stages (DB = 2), then 8 x 4 KiB
+constexpr int SMEM = OFF_EPI + 8 * 16 * 64 * 4;
+constexpr int NSTORE = 16;                            // epilogue 16-B stores per lane per tile
+PIPNET_DEV int swz(int r) { return (((r >> 2) & 3) << 4) | ((r & 1) << 2); }
+}  // namespace ppp
+
+PIPNET_DEV void tile_coords_id(const ConvParams& p, int id, int bm, int bn, int& m0, int& n0) {
+  const int nwg = p.mt * p.nt;
+  const int tile = xcd_remap(id, nwg);
+  const int gm = p.group_m;
+  const int group = tile / (gm * p.nt);
+  const int first_m = group * gm;
+  const int gsz = min(p.mt - first_m, gm);
+  const int in_group = tile - group * gm * p.nt;
+  m0 = (first_m + in_group % gsz) * bm;
+  n0 = (in_group / gsz) * bn;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) {
+  using namespace pp;
+  constexpr int DB = 2, NS = 4;
+  constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[ppp::SMEM];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int nk = p.K / BK;
+  const int ntiles = p.mt * p.nt;
+
+  const int drow = lane >> 2;
+  const int dchunk = 8 * ((lane & 3) ^ g(drow));
+  int64_t abase[2];
+  const bf16* wsrc[2];
+  auto setup = [&](int id, int& m0, int& n0) {
+    tile_coords_id(p, id, BM, BN, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 16 * (wid + 8 * i) + drow;
+      abase[i] = (int64_t)min(m0 + row, p.M - 1) * p.lda + dchunk;
+      wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
+    }
+  };
+  auto stage_a = [&](int kt) {
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+    const int k0 = seg_remap(p, min(kt * BK, p.Kv - BK));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + abase[i] + k0),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
+                                       0, 0);
+  };
+  auto stage_b = [&](int kt) {
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + BM * ROWB +
+                                                                                 (wid + 8 * i) * 1024),
+                                       16, 0, 0);
+  };
+  auto prologue_dma = [&]() {
+    stage_a(0), stage_b(0);
+    if (1 < nk) stage_a(1), stage_b(1);
+    if (2 < nk) stage_a(2);
+  };
+  const int fr = lane & 15;
+  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
+  auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
+  };
+  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
+#pragma unroll
+    for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 64 + n * 16) * ROWB + fofs);
+  };
+  auto younger_than_b = [&](int kt) {
+    return ((kt + 2 < nk) ? 4 : 0) + ((kt + 3 < nk) ? 2 : 0);
+  };
+
+  int m0, n0;
+  int id = blockIdx.x;
+  setup(id, m0, n0);
+  prologue_dma();
+  pp_wait_vm_dyn(younger_than_b(-1));
+  pp_barrier();
+  int extra = 0;                       // epilogue stores younger than this tile's first B(1)
+  for (;;) {
+    if (wr == 1) pp_barrier();         // group 1 runs one barrier behind
+    f32x4v acc[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    bf16x8v fa[4], fb[4];
+    auto ktile = [&](int kt, auto steady) {
+      constexpr bool STEADY = decltype(steady)::value;
+      const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+      if (STEADY || kt + DB < nk) stage_b(kt + DB);
+      read_b(fb, st);
+      read_a(fa, st, 0);
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      if (STEADY || kt + DB + 1 < nk) stage_a(kt + DB + 1);
+      read_a(fa, st, 1);
+      if constexpr (STEADY) pp_wait_vm<6>();
+      else pp_wait_vm_dyn(younger_than_b(kt));
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+    };
+    int kt = 0;
+    if (extra && nk > DB + 1) {        // first K-tile after a tile switch: the stores of the
+      const unsigned char* st = smem;  // previous epilogue sit between A(2) and B(2)
+      stage_b(DB);
+      read_b(fb, st);
+      read_a(fa, st, 0);
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      stage_a(DB + 1);
+      read_a(fa, st, 1);
+      pp_wait_vm<6 + ppp::NSTORE>();
+      pp_barrier();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+          acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      pp_barrier();
+      kt = 1;
+    }
+    for (; kt < nk - DB - 1; ++kt) ktile(kt, IntC<1>{});
+    for (; kt < nk; ++kt) ktile(kt, IntC<0>{});
+    if (wr == 0) pp_barrier();         // re-align the groups
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();                      // every wave is past its last stage read
+
+    // ---- next tile's first K-tiles go out before this tile's epilogue ----
+    const int cm0 = m0, cn0 = n0;
+    id += gridDim.x;
+    const bool more = id < ntiles;
+    if (more) {
+      setup(id, m0, n0);
+      prologue_dma();
+    }
+    // ---- epilogue: 8 pieces of 16 rows per wave through the wave's 4 KiB region ----
+    float* wt = reinterpret_cast<float*>(smem + ppp::OFF_EPI) + wid * 16 * 64;
+    const int c8 = lane & 7;
+    const int n = cn0 + wc * 64 + 8 * c8;
+    f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
+    if (EPI != PIPNET_EPI_NONE && p.bias) {
+      b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
+      b1 = *reinterpret_cast<const f32x4v*>(p.bias + n + 4);
+    }
+    bf16x8v rr[16];
+    if (HAS_R) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = min(cm0 + wr * 128 + q * 8 + (lane >> 3), p.M - 1);
+        rr[q] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
+      }
+    }
+    const int fq = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+#pragma unroll
+      for (int nn = 0; nn < 4; ++nn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = 4 * fq + i;
+          wt[row * 64 + ((nn * 16 + fr) ^ ppp::swz(row))] = acc[r][nn][i];
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int row = it * 8 + (lane >> 3);
+        const int sw = ppp::swz(row);
+        f32x4v x0 = *reinterpret_cast<const f32x4v*>(wt + row * 64 + ((8 * c8) ^ sw));
+        f32x4v x1 = *reinterpret_cast<const f32x4v*>(wt + row * 64 + ((8 * c8 + 4) ^ sw));
+        x0 += b0;
+        x1 += b1;
+        if (HAS_R) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            x0[e] += (float)rr[r * 2 + it][e];
+            x1[e] += (float)rr[r * 2 + it][4 + e];
+          }
+        }
+        if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            x0[e] = fmaxf(x0[e], 0.f);
+            x1[e] = fmaxf(x1[e], 0.f);
+          }
+        }
+        bf16x8v o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = (bf16)x0[e];
+          o[4 + e] = (bf16)x1[e];
+        }
+        const int m = min(cm0 + wr * 128 + r * 16 + row, p.M - 1);
+        *reinterpret_cast<bf16x8v*>(p.C + (int64_t)m * p.ldc + n) = o;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    if (!more) break;
+    // next tile's A(0) / B(0): younger are A1 B1 A2 (6) and this epilogue's stores (and, with a
+    // residual, its loads -- already consumed, hence retired with everything older)
+    if (nk > 2) pp_wait_vm<6 + ppp::NSTORE>();
+    else pp_wait_vm<ppp::NSTORE>();    // fewer than 6 pieces follow B(0): wait a little longer
+    pp_barrier();
+    extra = 1;
+  }
+}
+
+// ======================================================================================
 // 3x3 / stride 1 / pad 1 convolutions on the ping-pong tile with an LDS input halo.
 //
 // On the pp tile every 32-deep K-tile brings 16 KiB of A (256 pixels x 32 channels of one

@@ -134,6 +134,39 @@ def test_conv_bf16_halo(gpu, b, cin, cout, h, w, epi):
     _close_bf16(outs[0].cpu(), ref)
 
 
+@pytest.mark.parametrize("m,cin,cout,epi", [
+    (1083, 64, 256, _lib.EPI_BIAS_RESID_RELU),      # ragged M, 2 K-tiles (short-K path), one tile per WG
+    (1083, 96, 512, _lib.EPI_BIAS_RELU),            # K 96 -> 128 padded (re-read last A columns vs zero W)
+    (70000, 512, 512, _lib.EPI_BIAS_RESID_RELU),    # 548 tiles: several tiles per persistent workgroup
+    (70000, 256, 1024, _lib.EPI_BIAS),              # 1096 tiles, 8 K-tiles
+    (9000, 1024, 256, _lib.EPI_NONE),               # long K
+])
+def test_conv_bf16_persistent_pp(gpu, m, cin, cout, epi):
+    """Persistent ping-pong tile (tile 9, 1x1 convs with N % 256 == 0): same K order as the
+    pp tile, so bitwise equal to it -- including the tile switches, where the next tile's
+    first K-tiles are in flight during the previous epilogue -- and within one bf16 ulp of
+    the restated arithmetic."""
+    g = torch.Generator().manual_seed(m + cin + cout)
+    x = torch.randn(m, 1, 1, cin, generator=g).to(torch.bfloat16).to(gpu)
+    w = (torch.randn(cout, 1, 1, cin, generator=g) / cin ** 0.5).to(gpu)
+    wp = K.pack_conv_weight_bf16(w)
+    b = torch.randn(cout, generator=g).to(gpu)
+    r = torch.randn(m, 1, 1, cout, generator=g).to(torch.bfloat16).to(gpu) if epi == _lib.EPI_BIAS_RESID_RELU else None
+    bias = b if epi != _lib.EPI_NONE else None
+    outs = [K.conv2d_nhwc_bf16(x, wp, 1, 1, bias, 1, 0, epi, r, tile=t) for t in (5, 9)]
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    if m <= 9000:
+        y = x.double().view(m, cin) @ wp[:, :cin].double().t()
+        if bias is not None:
+            y = y + b.double()
+        if r is not None:
+            y = y + r.double().view(m, cout)
+        if epi in (_lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU):
+            y = torch.relu(y)
+        _close_bf16(outs[1].cpu().view(m, cout), _bf(y.float().cpu()))
+
+
 def test_conv_bf16_halo_batch_invariant(gpu):
     """The halo kernel's per-pixel arithmetic does not depend on the batch a pixel is in."""
     g = torch.Generator().manual_seed(5)
