@@ -1,6 +1,12 @@
 // Product instantiation of the fp32 MFMA GEMM (templates + design notes: gemm_f32_impl.hpp).
 #include "gemm_f32_impl.hpp"
 
+#include <cstdlib>
+
+#ifndef PIPNET_GEMM_PERSIST_DEFAULT
+#define PIPNET_GEMM_PERSIST_DEFAULT 0
+#endif
+
 using namespace pipnet_gemm;
 
 namespace {
@@ -51,6 +57,31 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// compute units of the current device, queried once
+int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// PIPNET_GEMM_PERSIST=0/1 (read once): the persistent 128x128 tile for variant-3 dense GEMMs
+// with N % 128 == 0 (A/B switch; the default is set from tools/gemm_bench.py runs).
+int g_gemm_persist = -1;
+bool gemm_persist() {
+  if (g_gemm_persist < 0) {
+    const char* e = getenv("PIPNET_GEMM_PERSIST");
+    g_gemm_persist = e ? (e[0] == '1') : PIPNET_GEMM_PERSIST_DEFAULT;
+  }
+  return g_gemm_persist == 1;
+}
+
 template <int ALOAD>
 int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   p.nt = (p.N + BN - 1) / BN;
@@ -62,6 +93,27 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   const int v = gemm_variant(p.M, p.N, p.K, vec);
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
+  if (ALOAD == ALOAD_DENSE && v == 3 && p.vec_epi && p.N % BN == 0 && gemm_persist()) {
+    const int ntiles = p.mt * p.nt;
+    const dim3 pgrid(ntiles < 2 * num_cus() ? ntiles : 2 * num_cus());
+#define PIPNET_PERSIST_CASE(E) \
+  case E: hipLaunchKernelGGL((gemm_f32_tn_persist_kernel<E>), pgrid, block, 0, s, p); break;
+    switch (epi) {
+      PIPNET_PERSIST_CASE(PIPNET_EPI_NONE)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_GELU)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_RESID)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_MUL)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_RELU)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_RESID_RELU)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_RESID_ROWSCALE)
+      PIPNET_PERSIST_CASE(PIPNET_EPI_GELU_BWD)
+      default: return PIPNET_ERR_ARG;
+    }
+#undef PIPNET_PERSIST_CASE
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
     if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
@@ -89,6 +141,12 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
 }
 
 }  // namespace
+
+extern "C" int pipnet_gemm_persist(int mode) {
+  if (mode == 0 || mode == 1) g_gemm_persist = mode;
+  else if (mode != -1) return PIPNET_ERR_ARG;
+  return gemm_persist() ? 1 : 0;
+}
 
 extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
                                  const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,

@@ -563,6 +563,167 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
 }
 
 // ======================================================================================
+// Persistent form of the 128x128 / BK 32 / 2-stage tile (dense A, N % 128 == 0, float4
+// epilogue).  Two workgroups per CU walk tiles blockIdx.x, +gridDim.x, ... of the same
+// XCD-grouped raster.  After a tile's last K-tile every wave has passed the loop's final
+// barrier, so both stages are free: the next tile's K-tile 0 is issued into stage 0 BEFORE
+// this tile's epilogue, which re-lays the accumulators through stage 1 with wave-local
+// ordering only (each wave owns 8 KiB of it; no workgroup barrier inside the epilogue).  The
+// epilogue's LDS accesses are inline asm: hipcc cannot tell that they miss the LDS-DMA's
+// stage and would otherwise drain that DMA (vmcnt(0)) before the first of them.  The bias /
+// scale / residual loads are issued before that DMA, and every lane stores exactly TM * 8
+// float4s (rows past M are clamped to row M-1, whose values they recompute from the clamped
+// A row -- identical bits), so one vmcnt(TM * 8) retires the next tile's K-tile 0 without
+// waiting for the stores.  What this removes per tile: the workgroup launch, the first
+// K-tile's load latency and the store drain of a retiring workgroup -- the per-tile gaps the
+// stamps saw as 1.76-1.88 resident workgroups per CU (of 2) on the stage-3/4 fc1 shapes.
+// ======================================================================================
+PIPNET_DEV void tile_coords_id(const GemmParams& p, int id, int bm, int& m0, int& n0) {
+  const int nwg = p.mt * p.nt;
+  const int tile = xcd_remap(id, nwg);
+  const int gm = p.group_m;
+  const int group = tile / (gm * p.nt);
+  const int first_m = group * gm;
+  const int gsz = min(p.mt - first_m, gm);
+  const int in_group = tile - group * gm * p.nt;
+  m0 = (first_m + in_group % gsz) * bm;
+  n0 = (in_group / gsz) * BN;
+}
+
+PIPNET_DEV unsigned lds_u32(const float* ptr) {
+  return (unsigned)(size_t)(const __attribute__((address_space(3))) float*)ptr;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(NTHREADS, 2) void gemm_f32_tn_persist_kernel(GemmParams p) {
+  constexpr int BK = 32, TM = 2;
+  using G = Geo<BK, TM>;
+  constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU ||
+                         EPI == PIPNET_EPI_RESID_ROWSCALE || EPI == PIPNET_EPI_GELU_BWD;
+  __shared__ __attribute__((aligned(16))) float smem[2 * G::TILE_FLOATS];
+  static_assert(G::TILE_FLOATS >= 4 * 32 * 64, "epilogue region = one stage");
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int nk = p.K / BK;
+  const int ntiles = p.mt * p.nt;
+  const int drow = lane / G::CHUNKS;
+  const float* asrc[G::A_DMA];
+  const float* wsrc[G::B_DMA];
+  auto setup = [&](int id, int& m0, int& n0) {
+    tile_coords_id(p, id, G::BMT, m0, n0);
+#pragma unroll
+    for (int i = 0; i < G::A_DMA; ++i) {
+      const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + drow;
+      asrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + 4 * G::swz(row, lane % G::CHUNKS);
+    }
+#pragma unroll
+    for (int i = 0; i < G::B_DMA; ++i) {
+      const int row = (i * NWAVES + wid) * G::ROWS_PER_DMA + drow;
+      wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 4 * G::swz(row, lane % G::CHUNKS);
+    }
+  };
+  auto stage = [&](int kt, int buf) {
+    float* base = smem + buf * G::TILE_FLOATS;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < G::A_DMA; ++i) dma16(asrc[i] + k0, base + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+#pragma unroll
+    for (int i = 0; i < G::B_DMA; ++i)
+      dma16(wsrc[i] + k0, base + G::BMT * BK + (i * NWAVES + wid) * G::ROWS_PER_DMA * BK);
+  };
+
+  int id = blockIdx.x, m0, n0;
+  setup(id, m0, n0);
+  stage(0, 0);
+  __syncthreads();
+  const int c4 = lane & 15;
+  // this wave's 8 KiB of stage 1: MFMA-layout writes at (row (v&3) + 8 (v>>2) + 4 lh, column
+  // j*32 + lr), float4 reads of row it*4 + (lane>>4), columns 4 c4 .. +3
+  const unsigned wt = lds_u32(smem + G::TILE_FLOATS + wid * 32 * 64);
+  const unsigned wa = wt + (unsigned)((4 * lh * 64 + lr) * 4);
+  const unsigned ra = wt + (unsigned)(((lane >> 4) * 64 + 4 * c4) * 4);
+  for (;;) {
+    Acc acc;
+    zero_acc(acc);
+    {
+      Frag fa, fb;
+      read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
+      int cur = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        const float* buf = smem + cur * G::TILE_FLOATS;
+        if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+        mfma_frag<TM>(acc, fa);
+        read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
+        mfma_frag<TM>(acc, fb);
+        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
+        mfma_frag<TM>(acc, fa);
+        __syncthreads();                                 // tile kt+1 landed, tile kt read
+        if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + (cur ^ 1) * G::TILE_FLOATS, wm, wn, lr, lh, 0);
+        mfma_frag<TM>(acc, fb);
+        cur ^= 1;
+      }
+    }
+    // ---- this tile's epilogue operands, then the next tile's K-tile 0, then the epilogue ----
+    const int cm0 = m0;
+    const int n = n0 + wn * 64 + 4 * c4;
+    f32x4 bn = {0.f, 0.f, 0.f, 0.f}, sn = {1.f, 1.f, 1.f, 1.f};
+    if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && EPI != PIPNET_EPI_GELU_BWD && p.bias) bn = ld4(p.bias + n);
+    if ((EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) && p.scale) sn = ld4(p.scale + n);
+    // bias / scale in registers before the DMA below: hipcc waits vmcnt(0) for any load still
+    // pending behind an LDS-DMA, which would drain the next tile's K-tile 0 here
+    asm volatile("" : "+v"(bn), "+v"(sn));
+    f32x4 r[TM][8];
+    if (HAS_R) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          const int m = min(cm0 + wm * 32 * TM + i * 32 + it * 4 + (lane >> 4), p.M - 1);
+          r[i][it] = ld4(p.R + (int64_t)m * p.ldr + n);
+        }
+    }
+    id += gridDim.x;
+    const bool more = id < ntiles;
+    // issued unconditionally (the last tile re-fetches its own K-tile 0, unused) so the number
+    // of VMEM ops in flight is the same on every path and hipcc's own waits for the epilogue
+    // operands above stay counted instead of falling back to vmcnt(0)
+    setup(more ? id : id - gridDim.x, m0, n0);
+    stage(0, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int v = 0; v < 16; ++v)
+          asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(wa), "v"(acc[i][j][v]),
+                       "i"((((v & 3) + 8 * (v >> 2)) * 64 + j * 32) * 4)
+                       : "memory");
+      f32x4 x[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it)
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(x[it]) : "v"(ra), "i"(it * 4 * 64 * 4) : "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int m = min(cm0 + wm * 32 * TM + i * 32 + it * 4 + (lane >> 4), p.M - 1);
+        float rs = 1.f;
+        if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[m / p.rows_per_scale];
+        st4_c(p.C + (int64_t)m * p.ldc + n, epi_math<EPI>(x[it], bn, sn, HAS_R ? r[i][it] : bn, rs));
+      }
+    }
+    if (!more) break;
+    // K-tile 0 of the next tile is older than exactly TM * 8 stores; every wave is done with
+    // its epilogue reads of stage 1 (lgkmcnt(0) above) before the barrier
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(TM * 8) : "memory");
+  }
+}
+
+// ======================================================================================
 // general path: register staging, zero-filled K tail (K % 4 == 0), 128x128x32 tiles
 // ======================================================================================
 constexpr int TBM = 128, TBK = 32, LDK = TBK + 4;   // padded rows (144 B): conflict-free ds_read_b128

@@ -44,7 +44,18 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     if n <= 384 or k <= 192 or m <= 64:
         npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
+    if aload == 0 and n % 128 == 0 and gemm_persist():
+        return f"pipnet_gemm::gemm_f32_tn_persist_kernel<{epilogue}>"
     return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
+
+
+def gemm_persist(mode: int = -1) -> bool:
+    """The library's persistent-GEMM switch (include/pipnet_amd.h pipnet_gemm_persist): mode 1 / 0
+    sets it, -1 queries."""
+    r = _lib.load().pipnet_gemm_persist(mode)
+    if r < 0:
+        _lib.check(r, f"pipnet_gemm_persist({mode})")
+    return bool(r)
 
 
 SPLITK_WG_PER_CU = int(os.environ.get("PIPNET_SPLITK_WG_PER_CU", "2"))   # env: A/B runs (tools)

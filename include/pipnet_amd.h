@@ -62,6 +62,12 @@ int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* 
                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                       int M, int N, int K, int epilogue, void* stream);
 
+/* Persistent 128x128 fp32 GEMM tile for the 128-row / 2-stage shapes with N % 128 == 0
+ * (stage-3/4 CNBlock Linears): mode 1 on, 0 off, -1 query only.  Returns the mode in force
+ * (initially PIPNET_GEMM_PERSIST from the environment, else the build default) or a
+ * negative status.  Not thread-safe against concurrent launches (process-wide A/B switch). */
+int pipnet_gemm_persist(int mode);
+
 /* pipnet_linear_f32 with PIPNET_EPI_RESID_ROWSCALE: C = R + row_scale[m / rows_per_scale] *
  * (scale * (A W^T + bias)).  The CNBlock's Linear2 * layer_scale + residual under
  * torchvision's StochasticDepth("row") in train mode: rows_per_scale = H*W (one factor per

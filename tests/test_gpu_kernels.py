@@ -322,3 +322,38 @@ def test_cnblock_mlp_batch_invariant(gpu, c, m):
         part = x[:rows].clone()
         K.cnblock_mlp(t[:rows].contiguous(), w1, b1, w2, b2, gm, part)
         assert torch.equal(part, full[:rows]), rows
+
+
+@pytest.mark.parametrize("m,n,k,epi", [
+    (46656 // 4, 1536, 384, "gelu"),     # stage-3 fc1 shape (quarter batch): several tiles per workgroup
+    (10000, 3072, 768, "gelu"),          # stage-4 fc1 shape, ragged M
+    (46656 // 4, 512, 1536, "resid"),    # residual epilogue on the persistent tile
+    (300, 256, 512, "none"),             # fewer tiles than workgroups
+])
+def test_gemm_persistent_bitwise(gpu, m, n, k, epi):
+    """The persistent fp32 GEMM tile (pipnet_gemm_persist) keeps the K order and the epilogue
+    arithmetic of the 128x128 tile: outputs bitwise equal, including across tile switches
+    (next tile's K-tile 0 in flight during the epilogue) and the clamped rows past M."""
+    g = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).to(gpu)
+    w = (torch.randn(n, k, generator=g) * 0.05).to(gpu)
+    b = torch.randn(n, generator=g).to(gpu)
+    s = torch.randn(n, generator=g).to(gpu)
+    r = torch.randn(m, n, generator=g).to(gpu)
+    e = {"gelu": _lib.EPI_BIAS_GELU, "resid": _lib.EPI_RESID, "none": _lib.EPI_NONE}[epi]
+    prev = K.gemm_persist()
+    try:
+        outs = []
+        for mode in (0, 1):
+            K.gemm_persist(mode)
+            outs.append(K.linear(a, w, b, e, scale=s, r=r if epi == "resid" else None))
+        torch.cuda.synchronize()
+    finally:
+        K.gemm_persist(int(prev))
+    assert torch.equal(outs[0], outs[1])
+    ref = a.double() @ w.double().t()
+    if epi == "gelu":
+        ref = torch.nn.functional.gelu(ref + b.double())
+    elif epi == "resid":
+        ref = r.double() + s.double() * (ref + b.double())
+    assert (outs[1].double() - ref).abs().max().item() < 1e-3
