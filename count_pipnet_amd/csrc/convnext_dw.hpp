@@ -106,17 +106,22 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
 #pragma unroll
     for (int i = 0; i < TX; ++i) acc[t][i] = bq;
 
+  // Input rows through a buffer resource spanning exactly one image row (W*C floats): the
+  // hardware range check returns zeros for the columns left / right of the image (a negative
+  // offset wraps past num_records), so the 7x7 halo needs no per-load branch or select -- a
+  // per-element "load or zero" made hipcc branch around every load (exec-masked blocks) and
+  // spend more issue slots on 64-bit address arithmetic than on the FMAs.
+  const int voff0 = ((px0 - 3) * C + 4 * q) * 4;
 #pragma unroll
   for (int ir = 0; ir < TY + 6; ++ir) {
     const int iy = oy0 + ir - 3;
     if (iy < 0 || iy >= H) continue;
-    const float* row = x + (((int64_t)b * H + iy) * W) * C + 4 * q;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(x + (((int64_t)b * H + iy) * W) * C), (short)0, W * C * 4, 0x00020000);
     f32x4 v[TX + 6];
 #pragma unroll
-    for (int r = 0; r < TX + 6; ++r) {
-      const int ix = px0 + r - 3;
-      v[r] = (ix >= 0 && ix < W) ? ld4(row + (int64_t)ix * C) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int r = 0; r < TX + 6; ++r)
+      v[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff0 + r * C * 4, 0, 0));
 #pragma unroll
     for (int t = 0; t < TY; ++t) {
       const int ky = ir - t;
