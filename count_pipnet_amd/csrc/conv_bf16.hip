@@ -66,12 +66,17 @@ bool is_s3_epi(int epi) {
   return epi == PIPNET_EPI_S3_GELU || epi == PIPNET_EPI_F32_BIAS || epi == PIPNET_EPI_F32_RESID;
 }
 
-// 3x3 / stride 1 / pad 1 convs whose halo fits the kernel's 320 LDS rows (256 + 2W + 2):
-// the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer choice, never M.
+// 3x3 / stride 1 / pad 1 convs with N >= 256 whose halo fits the kernel's 320 LDS rows
+// (256 + 2W + 2): the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer
+// choice, never M.
 bool halo_ok(const ConvParams& p, int epi) {
   return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
          p.seg == 0 && p.Cin % 64 == 0 && p.Wd <= 31 && p.N >= 256 && !is_s3_epi(epi);
 }
+// B fragments of 16 columns per wave.  Only the 256-wide tile is dispatched: the 64 / 128-wide
+// instantiations (4 / 8 MFMAs per phase) measured slower than tile 6 on layer1 conv2 (125 vs
+// 88 us) and +5 % on layer2 conv2 (profiles/r02/conv_bf16_halo_narrow.log).
+int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
@@ -81,7 +86,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pk = ALOAD == ALOAD_DENSE && pp_ok && p.N % 256 == 0 && !is_s3_epi(epi);
   if (v < 0) {
     v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
-    if (v == 5 && hk) v = 8;
+    if (hk) v = 8;
     else if (v == 5 && pk) v = 9;
   }
   if (v > 9 || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
@@ -105,22 +110,25 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }
-  if (v == 8) {                                  // 256 x 256 ping-pong with the LDS input halo
-    p.nt = (p.N + 255) / 256;
+  if (v == 8) {                                  // ping-pong with the LDS input halo, 256 x 64 NB
+    const int nb = halo_nb(p.N);
+    p.nt = (p.N + 64 * nb - 1) / (64 * nb);
     p.mt = (p.M + 255) / 256;
     p.group_m = choose_group_m(p.K);
     const dim3 grid(p.mt * p.nt);
+#define PIPNET_HALO(E)                                                                                \
+  case E:                                                                                              \
+    if (nb == 4) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4>), grid, dim3(512), 0, s, p);       \
+    else return PIPNET_ERR_ARG;                                                                        \
+    break;
     switch (epi) {
-      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE>), grid, dim3(512), 0, s, p); break;
-      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS>), grid, dim3(512), 0, s, p); break;
-      case PIPNET_EPI_BIAS_RELU:
-        hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(512), 0, s, p);
-        break;
-      case PIPNET_EPI_BIAS_RESID_RELU:
-        hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(512), 0, s, p);
-        break;
+      PIPNET_HALO(PIPNET_EPI_NONE)
+      PIPNET_HALO(PIPNET_EPI_BIAS)
+      PIPNET_HALO(PIPNET_EPI_BIAS_RELU)
+      PIPNET_HALO(PIPNET_EPI_BIAS_RESID_RELU)
       default: return PIPNET_ERR_ARG;
     }
+#undef PIPNET_HALO
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }

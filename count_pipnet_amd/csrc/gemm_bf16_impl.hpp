@@ -1028,49 +1028,71 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 // ======================================================================================
 namespace ph {
 constexpr int DB = 2, NS = DB + 2;
-constexpr int BSTAGE = pp::BN * pp::ROWB;             // 16 KiB: the B rows of one K-tile
-constexpr int HALO_ROWS = 320;                        // 20 DMA pieces of 16 rows per chunk
-constexpr int HALO_BYTES = HALO_ROWS * pp::ROWB;      // 20 KiB
-constexpr int OFF_HALO = NS * BSTAGE;                 // 4 halo slots: pair parity x chunk half
-constexpr int OFF_ZERO = OFF_HALO + 4 * HALO_BYTES;
-constexpr int SMEM = OFF_ZERO + 256 > pp::EPI_BYTES ? OFF_ZERO + 256 : pp::EPI_BYTES;
 PIPNET_DEV int hs(int r) { return ((r >> 2) & 1) << 1; }
+// NB = 16-column B fragments per wave: the tile is 256 x 64 NB.  The halo holds 320 rows
+// (W <= 31) beside the 256-wide B stages, 384 rows (W <= 63) beside the narrower ones.
+template <int NB>
+struct Lay {
+  static constexpr int BROWS = 64 * NB;                      // B rows of one K-tile
+  static constexpr int BSTAGE = BROWS * pp::ROWB;
+  static constexpr int HALO_ROWS = NB == 4 ? 320 : 384;
+  static constexpr int HPC = HALO_ROWS / 16;                 // DMA pieces per chunk half
+  static constexpr int HPW = 2 * HPC / 8;                    // halo pieces per wave per pair (5 / 6)
+  static constexpr int BPW = BROWS / 16 >= 8 ? BROWS / 16 / 8 : 1;   // B pieces per wave per K-tile
+  static constexpr int HALO_BYTES = HALO_ROWS * pp::ROWB;
+  static constexpr int OFF_HALO = NS * BSTAGE;               // 4 halo slots: pair parity x chunk half
+  static constexpr int OFF_ZERO = OFF_HALO + 4 * HALO_BYTES;
+  static constexpr int SMEM = OFF_ZERO + 256 > pp::EPI_BYTES ? OFF_ZERO + 256 : pp::EPI_BYTES;
+  static_assert(2 * HPC % 8 == 0, "halo pieces split evenly over 8 waves");
+};
 }  // namespace ph
 
-template <int EPI>
+template <int EPI, int NB = 4>
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
   using namespace pp;
   using ph::NS;
-  __shared__ __attribute__((aligned(256))) unsigned char smem[ph::SMEM];
+  using L = ph::Lay<NB>;
+  // The 64 / 128-wide forms (NB = 1 / 2: 384-row halo, duplicated B pieces) passed the
+  // kernel-level tests but measured slower / flat and failed the C3 end-to-end bf16 bound
+  // (pooled 0.10 vs 0.05) in their one run -- not dispatched, not validated.
+  static_assert(NB == 4, "only the 256-wide halo tile is validated");
+  constexpr int WCOLS = 16 * NB;
+  __shared__ __attribute__((aligned(256))) unsigned char smem[L::SMEM];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   int m0, n0;
-  tile_coords(p, BM, BN, m0, n0);
+  tile_coords(p, BM, L::BROWS, m0, n0);
   const int W = p.Wd, HW = p.H * p.Wd;
   const int npair = p.Cin / (2 * BK);
   const int nk = 18 * npair;
 
-  // ---- B DMA sources: pieces wid and wid + 8 (16 rows x 64 B each), pp swizzle ----
+  // ---- B DMA sources: BPW pieces of 16 rows x 64 B per wave (pp swizzle); with fewer pieces
+  // than waves (NB = 1: 4 pieces) waves 4..7 repeat waves 0..3's pieces -- identical bytes to the
+  // same LDS rows, so every wave issues the same count and the vmcnt waits stay uniform ----
   const int drow = lane >> 2;
-  const bf16* wsrc[2];
+  const bf16* wsrc[L::BPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * (wid + 8 * i) + drow;
+  for (int i = 0; i < L::BPW; ++i) {
+    const int pc = L::BROWS / 16 >= 8 ? wid + 8 * i : (wid % (L::BROWS / 16));
+    const int row = 16 * pc + drow;
     wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + 8 * ((lane & 3) ^ g(drow));
   }
-  // ---- halo DMA: 40 pieces per pair (20 per chunk half), 5 per wave: piece e = wid + 8 i is
-  // chunk half e / 20, halo rows 16 (e % 20) + ...; halo row i = pixel m0 - W - 1 + i ----
-  int64_t hsrc[5];
-  int hdst[5];
+  int bdst[L::BPW];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int e = wid + 8 * i, h = e >= 20 ? 1 : 0, pc = e - 20 * h;
+  for (int i = 0; i < L::BPW; ++i) bdst[i] = (L::BROWS / 16 >= 8 ? wid + 8 * i : (wid % (L::BROWS / 16))) * 1024;
+  // ---- halo DMA: 2 HPC pieces per pair, HPW per wave: piece e = wid + 8 i is chunk half
+  // e / HPC, halo rows 16 (e % HPC) + ...; halo row i = pixel m0 - W - 1 + i ----
+  int64_t hsrc[L::HPW];
+  int hdst[L::HPW];
+#pragma unroll
+  for (int i = 0; i < L::HPW; ++i) {
+    const int e = wid + 8 * i, h = e >= L::HPC ? 1 : 0, pc = e - L::HPC * h;
     const int row = 16 * pc + drow;
     const int pix = min(max(m0 - W - 1 + row, 0), p.M - 1);
     hsrc[i] = (int64_t)pix * p.Cin + h * BK + 8 * ((lane & 3) ^ ph::hs(row));
-    hdst[i] = h * ph::HALO_BYTES + pc * 1024;
+    hdst[i] = h * L::HALO_BYTES + pc * 1024;
   }
   // ---- this lane's 8 fragment rows: tile row wr*128 + j*16 + (lane & 15); 9-bit tap masks ----
   const int fr = lane & 15;
@@ -1091,32 +1113,32 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
     }
     vmask[j] = mk;
   }
-  if (tid < 16) *reinterpret_cast<u32x4*>(smem + ph::OFF_ZERO + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
+  if (tid < 16) *reinterpret_cast<u32x4*>(smem + L::OFF_ZERO + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 
   auto stage_b = [&](int kt) {
     const int P = kt / 18, rem = kt - 18 * P;
     const int k0 = (rem >> 1) * p.Cin + (2 * P + (rem & 1)) * BK;
-    unsigned char* base = smem + (kt % NS) * ph::BSTAGE;
+    unsigned char* base = smem + (kt % NS) * L::BSTAGE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < L::BPW; ++i)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + k0),
-                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
-                                       0, 0);
+                                       (__attribute__((address_space(3))) void*)(base + bdst[i]), 16, 0, 0);
   };
   auto stage_halo = [&](int P) {
-    unsigned char* base = smem + ph::OFF_HALO + (P & 1) * 2 * ph::HALO_BYTES;
+    unsigned char* base = smem + L::OFF_HALO + (P & 1) * 2 * L::HALO_BYTES;
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < L::HPW; ++i)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + hsrc[i] + P * 2 * BK),
                                        (__attribute__((address_space(3))) void*)(base + hdst[i]), 16, 0, 0);
   };
   const int fofs_b = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
   const int q16 = (lane >> 4) << 4;
-  auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
+  auto read_b = [&](bf16x8v (&fb)[NB], const unsigned char* st) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const bf16x8v*>(st + (wc * 64 + n * 16) * ROWB + fofs_b);
+    for (int n = 0; n < NB; ++n)
+      fb[n] = *reinterpret_cast<const bf16x8v*>(st + (wc * WCOLS + n * 16) * ROWB + fofs_b);
   };
-  const unsigned char* zb = smem + ph::OFF_ZERO;
+  const unsigned char* zb = smem + L::OFF_ZERO;
   // lane byte offset inside a halo slot for this tap (fragment rows j add j * 1 KiB)
   auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* hb, int half, int loff, unsigned tbit) {
     const unsigned char* zl = zb + (loff & 255);
@@ -1128,17 +1150,17 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
     }
   };
 
-  f32x4v acc[8][4];
+  f32x4v acc[8][NB];
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
   // prologue: halo(0), B(0), B(1); wait for halo(0) and B(0)
   stage_halo(0);
   stage_b(0);
   if (1 < nk) stage_b(1);
-  if (nk > 1) pp_wait_vm<2>();
+  if (nk > 1) pp_wait_vm<L::BPW>();
   else pp_wait_vm<0>();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // zero block written
   pp_barrier();
@@ -1149,12 +1171,12 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   // are B(kt+2) and the halo pieces issued at (0, 1) or, for (1, 0), one K-tile earlier; none
   // in the last tap of the last pair.  Everything but the MFMA stream is scalar bookkeeping
   // kept branch-light (one compile-time h per unrolled half).
-  bf16x8v fa[4], fb[4];
+  bf16x8v fa[4], fb[NB];
   const int lrow = wr * 128 + fr;
   int kt = 0;
   for (int P = 0; P < npair; ++P) {
     const bool more = P + 1 < npair;
-    const unsigned char* hp = smem + ph::OFF_HALO + (P & 1) * 2 * ph::HALO_BYTES;
+    const unsigned char* hp = smem + L::OFF_HALO + (P & 1) * 2 * L::HALO_BYTES;
     for (int t = 0; t < 9; ++t) {
       const int ky = t >= 6 ? 2 : (t >= 3 ? 1 : 0), kx = t - 3 * ky;
       const int hr = lrow + ky * W + kx;                       // this lane's halo row of fragment j = 0
@@ -1163,8 +1185,8 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
       const bool last = !more && t == 8;
 #pragma unroll
       for (int h = 0; h < 2; ++h, ++kt) {
-        const unsigned char* st = smem + (kt & (NS - 1)) * ph::BSTAGE;
-        const unsigned char* hb = hp + h * ph::HALO_BYTES;
+        const unsigned char* st = smem + (kt & (NS - 1)) * L::BSTAGE;
+        const unsigned char* hb = hp + h * L::HALO_BYTES;
         // ---- phase 0: rows 0..63 of the wave's block ----
         if (!last) stage_b(kt + 2);
         read_b(fb, st);
@@ -1174,7 +1196,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+          for (int n = 0; n < NB; ++n)
             acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
         pp_barrier();
@@ -1182,14 +1204,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
         if (h == 1 && t == 0 && more) stage_halo(P + 1);
         read_a(fa, hb, 1, loff, tbit);
         if (last) pp_wait_vm<0>();
-        else if (more && ((h == 1 && t == 0) || (h == 0 && t == 1))) pp_wait_vm<7>();
-        else pp_wait_vm<2>();
+        else if (more && ((h == 1 && t == 0) || (h == 0 && t == 1))) pp_wait_vm<L::BPW + L::HPW>();
+        else pp_wait_vm<L::BPW>();
         pp_barrier();
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int n = 0; n < 4; ++n)
+          for (int n = 0; n < NB; ++n)
             acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
         pp_barrier();
@@ -1199,7 +1221,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   if (wr == 0) pp_barrier();                                   // re-align the groups
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pp_barrier();                                                // stage / halo buffers free for the epilogue
-  pp_epilogue<EPI, 4>(p, acc, smem, m0, n0, wr, wc, lane, wid);
+  pp_epilogue<EPI, NB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
 }
 
 }  // namespace pipnet_bf16

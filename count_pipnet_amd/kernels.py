@@ -210,7 +210,7 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
                    ppp_ok: bool = False) -> int:
     """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
-    8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31),
+    8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31, N >= 256),
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
     MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
@@ -223,8 +223,10 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
         if n == 384:
             return 7 if kv >= 3 * 1024 else m128
         return 5 if n >= 256 else m128
+    if halo_ok:
+        return 8
     if n >= 256 and pp_ok:
-        return 8 if halo_ok else (9 if ppp_ok else 5)
+        return 9 if ppp_ok else 5
     if n <= 64 and not s3:
         return 6
     if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
@@ -244,7 +246,8 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 9:
         return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}>"
     if t == 8:
-        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}>"
+        nb = 4 if n >= 256 else (2 if n >= 128 else 1)
+        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, {nb}>"
     if t == 5:
         return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4, 0, 2>"
     if t == 7:
