@@ -58,7 +58,10 @@ def main():
         oh = (h + 2 * pad - k) // s + 1
         r = torch.randn(a.batch, oh, oh, cout, device=dev).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
         flops = 2.0 * a.batch * oh * oh * cout * k * k * cin
-        line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={K.bf16_conv_tile(a.batch * oh * oh, cout)}"
+        halo = k == 3 and s == 1 and pad == 1 and cin % 64 == 0 and oh <= 31 and cout >= 256
+        ppp = k == 1 and s == 1 and pad == 0 and cout % 256 == 0
+        auto = K.bf16_conv_tile(a.batch * oh * oh, cout, halo_ok=halo, ppp_ok=ppp)
+        line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={auto}"
         for t in tiles:
             try:
                 for _ in range(2):
