@@ -106,9 +106,23 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
   for (int j = 0; j < NV; ++j)
 #pragma unroll
     for (int e = 0; e < 8; ++e) racc[j][e] = 0.f;
-  for (int pi = wv; pi < PIX_PER_BLOCK; pi += HEAD_THREADS / 64) {
+  // the next pixel's logits are requested under the current one's math (one HBM latency per
+  // wave per pixel otherwise: the wave walks its pixels serially)
+  constexpr int STEP = HEAD_THREADS / 64;
+  bf16x8_t xc[NV], xn[NV];
+  auto load_pix = [&](int pix, bf16x8_t (&x)[NV]) {
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+      const int c = 8 * lane + 512 * j;
+      if (c < P) x[j] = *reinterpret_cast<const bf16x8_t*>(feat + base + c);
+    }
+  };
+  if (wv < PIX_PER_BLOCK && pix0 + wv < HW) load_pix(pix0 + wv, xc);
+  for (int pi = wv; pi < PIX_PER_BLOCK; pi += STEP) {
     const int pix = pix0 + pi;
     if (pix >= HW) break;
+    if (pi + STEP < PIX_PER_BLOCK && pix + STEP < HW) load_pix(pix + STEP, xn);
     const int64_t base = ((int64_t)b * HW + pix) * P;
     float v[NV][8];
     float m = -INFINITY;
@@ -116,7 +130,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
     for (int j = 0; j < NV; ++j) {
       const int c = 8 * lane + 512 * j;
       if (c < P) {
-        const bf16x8_t x = *reinterpret_cast<const bf16x8_t*>(feat + base + c);
+        const bf16x8_t x = xc[j];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[j][e] = (float)x[e], m = fmaxf(m, v[j][e]);
       } else {
@@ -150,6 +164,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
         }
       }
     }
+#pragma unroll
+    for (int j = 0; j < NV; ++j) xc[j] = xn[j];
   }
 #pragma unroll
   for (int j = 0; j < NV; ++j)
