@@ -1,12 +1,22 @@
 """Throughput of the MI355X PIP-Net inference path (BASELINE.json metric).
 
 A "step" = one ``PIPNet.forward(xs, inference=True)`` of ConvNeXt-tiny-26 over one batch of
-64 synthetic 224x224 images per GPU (CUB-200 shape, 200 classes, fp32), inputs resident in
-HBM, plus -- for N > 1 -- the RCCL all-gather of logits and pooled presence over xGMI that
-replaces nn.DataParallel's gather (main.py:118).  Weak scaling: 64 images per GPU.
+64 synthetic 224x224 images per GPU (fp32), inputs resident in HBM, plus -- for N > 1 -- the
+RCCL all-gather of logits and pooled presence over xGMI that replaces nn.DataParallel's
+gather (main.py:118).  Weak scaling: 64 images per GPU.  200 classes (CUB-200, BASELINE
+configs[1]) except at N = 8, where the workload is configs[3] (CARS: 196 classes, 512 images
+over 8 GPUs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
-    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--no-extra]
+
+With ``--gpus N > 1`` and no torchrun environment, bench.py launches its own N ranks (a
+``torch.distributed.run`` child, started before anything touches the GPU) and exits with
+its status; under torchrun, ``WORLD_SIZE`` must equal N.
+
+The same run also times the other GPU configs of BASELINE.json on each rank's shard
+(``extra``): C3 (PIP-Net ResNet-50, 128 images of 224x224, bf16) and C5 (CountPIPNet
+bilinear, 2048 prototypes, 64 images of 128x128 per GPU; BASELINE configs[4] shards 256
+over 4 GPUs), each with its own dominant-kernel roofline.  ``value`` / ``config`` stay C2.
 
 Prints one JSON line on rank 0 (fields described in DESIGN.md section "Measurement").
 """
@@ -17,6 +27,8 @@ import contextlib
 import io
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +42,56 @@ METRIC = "images/sec fwd, CUB-200 224×224 bs=64 ConvNeXt-tiny, 1/2/4/8 MI355X"
 PEAK_F32_TFLOPS = 157.3          # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, spec
 PEAK_HBM_GBS = 8000.0
 PEAK_BF16_TFLOPS = 2500.0        # MI355X_MICROARCH.md: BF16 dense matrix peak
+GFLOP_C2 = 40.094159616          # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--classes", type=int, default=None,
+                    help="classifier width (default: 196 = CARS at N = 8, BASELINE configs[3]; else 200 = CUB)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / C5 timings")
+    ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
+                    help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
+    ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
+                    help="also time this precision on the same network (reported under alt_precision)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="rehearsal only: torch.distributed backend (default nccl = RCCL on GPUs)")
+    ap.add_argument("--device-index", type=int, default=None,
+                    help="rehearsal only: put every rank on this GPU (multi-rank runs on a 1-GPU box)")
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks_if_needed(a) -> None:
+    """``--gpus N`` is authoritative.  Under torchrun (WORLD_SIZE set) it must match the world
+    size; without it and N > 1, start N ranks as a ``torch.distributed.run`` child process
+    (one process per GPU, RCCL over xGMI) and exit with its status.  Nothing here touches the
+    GPU, so the parent never holds a HIP context while its ranks run."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != a.gpus:
+            raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={ws} (torchrun's world size); "
+                             "they must agree")
+        return
+    if a.gpus <= 1:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.run(cmd, env=env).returncode)
 
 
 def make_net(device, num_classes=200, precision="fp32"):
@@ -43,8 +105,40 @@ def make_net(device, num_classes=200, precision="fp32"):
     return net.eval().to(device), args
 
 
+# the other GPU configs of BASELINE.json, timed per rank after the headline (tools/bench_configs.py
+# holds the same definitions for stand-alone runs)
+EXTRA = {
+    "c3": dict(baseline="configs[2]", model="pipnet", batch=128, size=224, classes=200, gflop=38.16,
+               dtype="bf16", peak=PEAK_BF16_TFLOPS,
+               workload="PIP-Net ResNet-50 forward(inference=True), 224x224, 200 classes, bf16 activations / "
+                        "weights with fp32 accumulation, 128 images per GPU",
+               args=dict(net="resnet50", num_features=0, bias=False, hip_dtype="bf16")),
+    "c5": dict(baseline="configs[4]", model="count", batch=64, size=128, classes=9, gflop=1.374,
+               dtype="f32", peak=PEAK_F32_TFLOPS,
+               workload="CountPIPNet bilinear forward(inference=True), 2048 prototypes, hard Gumbel head "
+                        "(Philox noise), 128x128, 9 classes, 64 images per GPU (configs[4]: 256 over 4 GPUs)",
+               args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=2048,
+                         activation="gumbel_softmax", intermediate_layer="bilinear", max_count=3, use_ste=True,
+                         bias=False)),
+}
+
+
+def make_extra(cfg, dev):
+    from count_pipnet_amd.count_pipnet import get_count_network
+    from count_pipnet_amd.pipnet import get_pipnet
+    from count_pipnet_amd.synthetic import fill_module_
+    a = argparse.Namespace(disable_pretrained=True, backward_clamp_strategy="Gated", **cfg["args"])
+    with contextlib.redirect_stdout(io.StringIO()):
+        if cfg["model"] == "pipnet":
+            net, _ = get_pipnet(cfg["classes"], a)
+        else:
+            net, _ = get_count_network(cfg["classes"], a, max_count=a.max_count, use_ste=a.use_ste)
+    fill_module_(net, 7, "trained")
+    return net.eval().to(dev)
+
+
 class GemmTimer:
-    """Brackets every MFMA GEMM launch with HIP events on the launching stream."""
+    """Brackets every MFMA GEMM / conv launch with HIP events on the launching stream."""
 
     def __init__(self):
         self.rec = []
@@ -91,7 +185,6 @@ def measured_traffic(dom):
 
 def _cpu_model():
     try:
-        import subprocess
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
             if line.startswith("Model name:"):
@@ -101,76 +194,105 @@ def _cpu_model():
     return "unknown"
 
 
+def host_cpu_share():
+    """The host cores this process may actually use: its scheduler affinity and its cgroup
+    CPU quota (v2 ``cpu.max`` or v1 ``cpu.cfs_quota_us / cpu.cfs_period_us``).  Returns
+    (cores, affinity, quota_cpus or None, source)."""
+    aff = len(os.sched_getaffinity(0))
+    quota, src = None, "no cgroup CPU quota found"
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, p = f.read().split()[:2]
+            if q != "max":
+                quota, src = float(q) / float(p), f"{path} = {q} {p}"
+            else:
+                src = f"{path} = max"
+            break
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota, src = q / p, f"cgroup v1 cfs_quota_us/cfs_period_us = {q}/{p}"
+        except (OSError, ValueError):
+            pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return cores, aff, quota, src
+
+
 def cpu_baseline(batch=64, repeats=3):
     """The oracle (pure-torch CPU restatement of the reference forward, parity-pinned to the
     reference's goldens) on the host cores, by SURVEY.md 8(d) / BASELINE.md's protocol:
     the same 64-image 224x224 batch as the GPU step, 1 warm-up forward, then the median of
-    3 timed forwards.  Reports nproc, the lscpu model name and torch's thread count."""
+    3 timed forwards, on as many torch threads as the process has host cores (affinity and
+    cgroup quota)."""
     import statistics
     from oracle import ref_cpu
     from count_pipnet_amd.synthetic import synth_images
-    net, args = make_net(torch.device("cpu"))
-    sd = {k: v for k, v in net.state_dict().items()}
-    xs = synth_images(batch, 224, seed=1)
-    times = []
-    with torch.no_grad():
-        ref_cpu.pipnet_forward(xs, sd, args, inference=True)       # warm-up
-        for _ in range(repeats):
-            t0 = time.perf_counter()
-            ref_cpu.pipnet_forward(xs, sd, args, inference=True)
-            times.append(time.perf_counter() - t0)
+    cores, aff, quota, src = host_cpu_share()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        net, args = make_net(torch.device("cpu"))
+        sd = {k: v for k, v in net.state_dict().items()}
+        xs = synth_images(batch, 224, seed=1)
+        times = []
+        with torch.no_grad():
+            ref_cpu.pipnet_forward(xs, sd, args, inference=True)       # warm-up
+            for _ in range(repeats):
+                t0 = time.perf_counter()
+                ref_cpu.pipnet_forward(xs, sd, args, inference=True)
+                times.append(time.perf_counter() - t0)
+        threads = torch.get_num_threads()
+    finally:
+        torch.set_num_threads(prev)
     med = statistics.median(times)
-    threads = torch.get_num_threads()
     return {"value": batch / med, "unit": "images/sec", "cores": threads, "kind": "port",
+            "affinity_cpus": aff, "cgroup_quota_cpus": quota, "quota_source": src,
             "nproc": os.cpu_count(), "cpu_model": _cpu_model(), "torch_threads": threads,
             "batch_seconds": times,
             "sample": f"one {batch}-image 224x224 batch (ConvNeXt-tiny-26 PIP-Net fp32, inference=True), "
                       f"1 warm-up + median of {repeats} = {med:.2f} s/batch; oracle/ref_cpu.py pipnet_forward "
-                      f"on {threads} torch threads; nproc={os.cpu_count()}, CPU: {_cpu_model()}"}
+                      f"on {threads} torch threads = the process's host-core share (affinity {aff} CPUs, "
+                      f"cgroup quota {quota if quota is not None else 'none'}); nproc={os.cpu_count()}, "
+                      f"CPU: {_cpu_model()}"}
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "bf16x3"], default="fp32",
-                    help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
-    ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
-                    help="also time this precision on the same network (reported under alt_precision)")
-    ap.add_argument("--dist-backend", default=None,
-                    help="rehearsal only: torch.distributed backend (default nccl = RCCL on GPUs)")
-    ap.add_argument("--device-index", type=int, default=None,
-                    help="rehearsal only: put every rank on this GPU (multi-rank runs on a 1-GPU box)")
-    a = ap.parse_args()
+    a = parse_args()
+    launch_ranks_if_needed(a)
 
     from count_pipnet_amd import build, kernels
     from count_pipnet_amd.dist import ShardedInference, init_from_env
     rank, world, dev = init_from_env(a.dist_backend, a.device_index)
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but the process group has {world} ranks")
     build.build()
     from count_pipnet_amd.synthetic import synth_images
-    net, _ = make_net(dev, precision=a.precision)
+    classes = a.classes if a.classes is not None else (196 if world == 8 else 200)
+    net, _ = make_net(dev, num_classes=classes, precision=a.precision)
     # one process per GPU, weights resident, this rank's 64-image shard already in HBM; the
     # step ends with the RCCL all-gather of pooled + logits (DataParallel's gather)
     sharded = ShardedInference(net)
     xs = synth_images(a.batch, 224, seed=100 + rank).to(dev)
 
-    def step():
-        with torch.no_grad():
-            _, pooled, out = sharded(xs, inference=True, global_batch=False, sizes=[a.batch] * world)
-        return out
-
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def timed():
-        """W warm-up steps, then K steps bracketed by barrier + synchronize; every MFMA GEMM
-        launch in the timed region is bracketed by HIP events on the stream it is launched
+    def timed(model, inp, batch, steps, warmup):
+        """W warm-up steps, then K steps bracketed by barrier + synchronize; every MFMA GEMM /
+        conv launch in the timed region is bracketed by HIP events on the stream it is launched
         on (torch's current stream) for the dominant-kernel roofline.  Max over ranks."""
-        for _ in range(a.warmup):
+        def step():
+            with torch.no_grad():
+                model(inp, inference=True, global_batch=False, sizes=[batch] * world)
+        for _ in range(warmup):
             step()
         timer = GemmTimer()
         kernels.set_launch_hook(timer)
@@ -179,7 +301,7 @@ def main():
         torch.cuda.synchronize()
         timer.enabled = True
         t0 = time.perf_counter()
-        for _ in range(a.steps):
+        for _ in range(steps):
             step()
         torch.cuda.synchronize()
         barrier()
@@ -193,24 +315,28 @@ def main():
             elapsed = float(t.item())
         return elapsed, timer.summary()
 
-    def roofline(agg, split):
+    def roofline(agg, steps, peak_of):
         dom = max(agg, key=lambda k: agg[k][2])
         n_l, fl, tt = agg[dom]
-        # split-bf16 GEMMs run 3 bf16 products per fp32 product: their fp32-equivalent ceiling
-        # is the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
-        peak = PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
+        peak = peak_of(dom)
         return dom, {"bound": "mfma", "kernel": dom, "achieved": fl / tt / 1e12, "peak": peak, "unit": "TFLOP/s",
-                     "frac": fl / tt / 1e12 / peak, "traffic": None, "launches_per_step": n_l / a.steps,
+                     "frac": fl / tt / 1e12 / peak, "traffic": None, "launches_per_step": n_l / steps,
                      "avg_launch_us": tt / n_l * 1e6, "algorithmic_gflop_per_launch": fl / n_l / 1e9}
 
-    gflop_img = 40.094159616       # oracle.ref_cpu.gflop_per_image(convnext_tiny_26, 224)
-    elapsed, agg = timed()
+    def peak_for(split):
+        # split-bf16 GEMMs run 3 bf16 products per fp32 product: their fp32-equivalent ceiling
+        # is the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
+        return lambda dom: PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
+
+    elapsed, agg = timed(sharded, xs, a.batch, a.steps, a.warmup)
     split = a.precision == "bf16x3"
-    dom, roof = roofline(agg, split)
+    dom, roof = roofline(agg, a.steps, peak_for(split))
     gemm_flops = sum(v[1] for v in agg.values())
     gemm_time = sum(v[2] for v in agg.values())
     imgs = a.batch * world * a.steps
     ms = elapsed / a.steps * 1e3
+    cfg_name = "configs[3]: CARS, 196 classes, 512 images over 8 GPUs" if (world == 8 and classes == 196) \
+        else f"configs[1]: CUB-200, {classes} classes"
     result = {
         "metric": METRIC,
         "value": imgs / elapsed,
@@ -224,32 +350,66 @@ def main():
         "vs_baseline": None,
         "dtype": "f32 (bf16x3 split-product GEMMs)" if split else "f32",
         "data": "synthetic",
-        "config": {"workload": "PIP-Net ConvNeXt-tiny-26 forward(inference=True), 224x224, 200 classes, fp32 "
-                               "(BASELINE configs[1]; configs[3] at N=8)" + (", split-bf16 GEMMs" if split else ""),
-                   "global_batch": a.batch * world, "per_gpu_batch": a.batch, "image_size": 224,
-                   "parallelism": f"dp{world}", "exchange": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+        "config": {"workload": f"PIP-Net ConvNeXt-tiny-26 forward(inference=True), 224x224, fp32, "
+                               f"BASELINE {cfg_name}" + (", split-bf16 GEMMs" if split else ""),
+                   "num_classes": classes, "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                   "image_size": 224, "parallelism": f"dp{world}",
+                   "exchange": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
                                 + " all_gather(logits, pooled)") if world > 1 else None},
         "roofline": roof,
-        "model_tflops": gflop_img * a.batch * world / (ms * 1e-3) / 1e3 / world,
-        "model_frac_of_f32_peak": gflop_img * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,
+        "model_tflops": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3,
+        "model_frac_of_f32_peak": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,
         "gemm_all": {"tflops": gemm_flops / gemm_time / 1e12, "ms_per_step": gemm_time / a.steps * 1e3},
     }
+    result["roofline"]["traffic"], result["roofline"]["traffic_source"] = measured_traffic(dom)
     if a.alt_precision != "none" and a.alt_precision != a.precision:
         # the same network and inputs with the other GEMM precision, timed the same way
         from count_pipnet_amd.pipnet import set_hip_dtype
         set_hip_dtype(net, a.alt_precision)
-        el2, agg2 = timed()
-        _, roof2 = roofline(agg2, a.alt_precision == "bf16x3")
+        el2, agg2 = timed(sharded, xs, a.batch, a.steps, a.warmup)
+        _, roof2 = roofline(agg2, a.steps, peak_for(a.alt_precision == "bf16x3"))
         ms2 = el2 / a.steps * 1e3
         result["alt_precision"] = {
             "precision": a.alt_precision,
             "dtype": "f32 (bf16x3 split-product GEMMs)" if a.alt_precision == "bf16x3" else "f32",
             "value": imgs / el2, "ms_per_step": ms2, "roofline": roof2,
-            "model_tflops_f32_equivalent": gflop_img * a.batch / (ms2 * 1e-3) / 1e3,
+            "model_tflops_f32_equivalent": GFLOP_C2 * a.batch / (ms2 * 1e-3) / 1e3,
             "accuracy": "fp32 inputs/outputs and accumulation; products of hi+lo bf16 splits (~1e-5 relative "
                         "per product); parity vs the reference goldens at the north-star 1e-3 "
                         "(tests/test_gpu_parity.py::test_hip_bf16x3_*)" if a.alt_precision == "bf16x3" else "exact"}
-    result["roofline"]["traffic"], result["roofline"]["traffic_source"] = measured_traffic(dom)
+    del sharded, net, xs
+    torch.cuda.empty_cache()
+
+    if not a.no_extra:
+        from count_pipnet_amd.pipnet import set_stream_split, stream_split
+        extra = {}
+        for name, cfg in EXTRA.items():
+            enet = make_extra(cfg, dev)
+            ewrap = ShardedInference(enet)
+            exs = synth_images(cfg["batch"], cfg["size"], seed=200 + rank).to(dev)
+            # throughput with the model's default stream split (C3: two half-batch streams)
+            nsplit = stream_split(enet, exs) if hasattr(enet, "_hip_logits") else 1
+            esteps = max(a.steps, 10)
+            el, eagg = timed(ewrap, exs, cfg["batch"], esteps, a.warmup)
+            rec = {"baseline": cfg["baseline"], "workload": cfg["workload"], "dtype": cfg["dtype"],
+                   "per_gpu_batch": cfg["batch"], "global_batch": cfg["batch"] * world, "image_size": cfg["size"],
+                   "value": cfg["batch"] * world * esteps / el, "unit": "images/sec",
+                   "ms_per_step": el / esteps * 1e3, "steps": esteps, "stream_split": nsplit,
+                   "model_tflops": cfg["gflop"] * cfg["batch"] / (el / esteps) / 1e3,
+                   "model_frac_of_peak": cfg["gflop"] * cfg["batch"] / (el / esteps) / 1e3 / cfg["peak"]}
+            if nsplit > 1:
+                # per-kernel durations of co-running streams overlap: the roofline comes from a
+                # one-stream pass over the same inputs
+                set_stream_split(enet, 1)
+                el1, eagg = timed(ewrap, exs, cfg["batch"], esteps, a.warmup)
+                set_stream_split(enet, nsplit)
+                rec["one_stream_ms_per_step"] = el1 / esteps * 1e3
+                rec["roofline_pass"] = "one stream (per-kernel events do not overlap another stream's kernels)"
+            _, rec["roofline"] = roofline(eagg, esteps, lambda dom, p=cfg["peak"]: p)
+            extra[name] = rec
+            del ewrap, enet, exs
+            torch.cuda.empty_cache()
+        result["extra"] = extra
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline()
     if rank == 0:

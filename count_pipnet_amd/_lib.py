@@ -99,6 +99,8 @@ EPI_RESID_ROWSCALE = 7
 EPI_GELU_BWD = 8
 EPI_S3_GELU, EPI_F32_BIAS, EPI_F32_RESID = 9, 10, 11      # split-bf16 ("bf16x3") ConvNeXt path
 
+ABI_VERSION = 2          # include/pipnet_amd.h PIPNET_AMD_ABI_VERSION
+
 _lib = None
 
 
@@ -122,6 +124,9 @@ def load() -> ctypes.CDLL:
         fn.argtypes = args
         fn.restype = _RESTYPE.get(name, ctypes.c_int)
     _check_provenance(lib)
+    if lib.pipnet_amd_abi_version() != ABI_VERSION:
+        raise PipnetLibraryError(f"{LIB_PATH} exports ABI version {lib.pipnet_amd_abi_version()}, "
+                                 f"this binding expects {ABI_VERSION} (include/pipnet_amd.h)")
     _lib = lib
     return lib
 

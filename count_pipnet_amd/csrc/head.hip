@@ -678,7 +678,7 @@ extern "C" int pipnet_count_encode_f32(const float* x, int B, int P, int C, int 
   return PIPNET_OK;
 }
 
-extern "C" int pipnet_amd_abi_version(void) { return 1; }
+extern "C" int pipnet_amd_abi_version(void) { return PIPNET_AMD_ABI_VERSION; }
 
 // sha256 over the library's sources (csrc/*.hip, csrc/*.hpp, include/*.h), computed by
 // count_pipnet_amd/build.py and passed on the hipcc line; _lib.load() compares it with the

@@ -10,11 +10,14 @@ gathers all three outputs back to GPU 0.  Here:
     dim 0, so shard sizes and order match), or each rank passes its own shard;
   * the only exchange is one all-gather of ``pooled`` [B/N, P] and ``out`` [B/N, K]
     over RCCL/xGMI -- no reduction is needed because images are independent (SURVEY.md 8e);
-  * ``proto_features`` is gathered too when the caller uses DataParallel's call pattern
-    (the full batch on every rank), because DataParallel gathers all three outputs and
-    callers index ``proto_features[i]`` across the batch (util/vis_pipnet.py:25).  Callers
-    that pass their own shard (``global_batch=False``, e.g. bench.py) get their shard's map
-    unless they ask for the gather.
+  * ``proto_features`` is gathered to rank 0 when the caller uses DataParallel's call
+    pattern (the full batch on every rank): DataParallel gathers all three outputs to
+    ``device_ids[0]`` and callers index ``proto_features[i]`` across the batch
+    (util/vis_pipnet.py:25).  Other ranks keep their own shard's map, so the map (133 MB per
+    64 ConvNeXt images) crosses xGMI once per shard, not once per rank pair.
+    ``gather_proto=True`` all-gathers it to every rank, ``False`` never gathers; callers that
+    pass their own shard (``global_batch=False``, e.g. bench.py) get their shard's map
+    unless they ask.
 
 ``ShardedInference`` keeps DataParallel's ``.module`` attribute, so callers written for
 the reference (``net.module._classification``, ``net.module._num_classes`` in
@@ -45,18 +48,38 @@ def shard_sizes(batch: int, world: int) -> List[int]:
     return sizes
 
 
+def _pad_rows(x: Tensor, rows: int) -> Tensor:
+    if x.shape[0] < rows:
+        pad = torch.zeros((rows - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        x = torch.cat([x, pad], dim=0)
+    return x.contiguous()
+
+
+def gather_rows_to_root(x: Tensor, sizes: List[int], group=None, root: int = 0) -> Tensor:
+    """Rank ``root`` receives every rank's rows concatenated in rank order; the other ranks
+    get their own ``x`` back (DataParallel's gather places the outputs on one device)."""
+    world = len(sizes)
+    if world == 1:
+        return x
+    xp = _pad_rows(x, max(sizes))
+    me = dist.get_rank(group)
+    bufs = [torch.empty_like(xp) for _ in range(world)] if me == root else None
+    dist.gather(xp, gather_list=bufs, dst=dist.get_global_rank(group, root) if group is not None else root,
+                group=group)
+    if me != root:
+        return x
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+
+
 def all_gather_rows(x: Tensor, sizes: List[int], group=None) -> Tensor:
     """Concatenate every rank's ``x`` (rank r holds ``sizes[r]`` rows) on every rank.
     Uneven shards are padded to the largest one for the collective and trimmed after."""
     world = len(sizes)
     if world == 1:
         return x
-    mx = max(sizes)
-    if x.shape[0] < mx:
-        pad = torch.zeros((mx - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        x = torch.cat([x, pad], dim=0)
+    x = _pad_rows(x, max(sizes))
     bufs = [torch.empty_like(x) for _ in range(world)]
-    dist.all_gather(bufs, x.contiguous(), group=group)
+    dist.all_gather(bufs, x, group=group)
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
 
 
@@ -83,9 +106,9 @@ class ShardedInference(nn.Module):
         pattern) and this rank takes its ``torch.chunk`` shard.  ``False``: ``xs`` is this
         rank's own shard (pass ``sizes`` -- every rank's shard size -- to skip the size
         exchange and its host sync).  Returns (proto_features, pooled [B, P], out [B, K]) in global
-        batch order; proto_features covers the whole batch when ``gather_proto`` is True, or
-        when it is None (the default) and ``global_batch`` is True -- DataParallel's outputs --,
-        and this rank's shard otherwise."""
+        batch order.  proto_features covers the whole batch on every rank when ``gather_proto``
+        is True; on rank 0 only when it is None (the default) and ``global_batch`` is True --
+        DataParallel's output placement --; and is this rank's shard otherwise."""
         world, rank = self.world, self.rank
         if global_batch:
             sizes = shard_sizes(xs.shape[0], world)
@@ -107,20 +130,23 @@ class ShardedInference(nn.Module):
         proto, pooled, out = self.module(local, inference=inference)
         pooled = all_gather_rows(pooled, sizes, self.process_group)
         out = all_gather_rows(out, sizes, self.process_group)
-        gather_proto = global_batch if self.gather_proto is None else self.gather_proto
-        if gather_proto and world > 1:
-            proto = gather_proto_features(proto, sizes, self.process_group)
+        if world > 1:
+            if self.gather_proto is None and global_batch:
+                proto = gather_proto_features(proto, sizes, self.process_group, to_root=True)
+            elif self.gather_proto:
+                proto = gather_proto_features(proto, sizes, self.process_group)
         return proto, pooled, out
 
 
-def gather_proto_features(proto: Tensor, sizes: List[int], group=None) -> Tensor:
-    """All-gather a [b, P, h, w] prototype map.  The HIP path returns it as a view of NHWC
-    storage (channels_last strides); it is exchanged in that storage order (no transpose
-    on either side) and handed back with the same strides."""
+def gather_proto_features(proto: Tensor, sizes: List[int], group=None, to_root: bool = False) -> Tensor:
+    """Gather a [b, P, h, w] prototype map to every rank (or to rank 0 with ``to_root``).  The
+    HIP path returns it as a view of NHWC storage (channels_last strides); it is exchanged in
+    that storage order (no transpose on either side) and handed back with the same strides."""
+    gather = gather_rows_to_root if to_root else all_gather_rows
     if proto.dim() == 4 and proto.permute(0, 2, 3, 1).is_contiguous():
-        g = all_gather_rows(proto.permute(0, 2, 3, 1), sizes, group)
+        g = gather(proto.permute(0, 2, 3, 1), sizes, group)
         return g.permute(0, 3, 1, 2)
-    return all_gather_rows(proto.contiguous(), sizes, group)
+    return gather(proto.contiguous(), sizes, group)
 
 
 def init_from_env(backend: Optional[str] = None, device_index: Optional[int] = None) -> Tuple[int, int, torch.device]:

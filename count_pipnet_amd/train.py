@@ -107,13 +107,24 @@ def hip_finetune_supported(net: nn.Module) -> bool:
     return {id(p) for p in m.parameters() if p.requires_grad} <= allowed
 
 
-def train_forward_hip(net: nn.Module, xs: Tensor, sd_keep: Optional[Dict[int, Tensor]]):
+def train_forward_hip(net: nn.Module, xs: Tensor, sd_keep: Optional[Dict[int, Tensor]],
+                      update_bn_stats: bool = True):
     """PIPNet.forward(xs, inference=False) with train-mode stochastic depth on the HIP
-    kernels: (proto NHWC [B,h,w,P], pooled [B,P], out [B,K])."""
+    kernels: (proto NHWC [B,h,w,P], pooled [B,P], out [B,K]).  Like the module's own forward
+    under ``net.train()``, a ResNet backbone's BatchNorms normalise with batch statistics and
+    take the running-statistics update; ``update_bn_stats=False`` restores every running
+    statistic and counter afterwards (an observer forward that must not advance them)."""
     from .pipnet import add_on_logits_hip
     m = _inner(net)
+    saved = None
+    if not update_bn_stats:
+        saved = [(b, b.clone()) for b in m._net.buffers()]
     with torch.no_grad():
-        feats = _backbone_train_forward(m, xs, sd_keep)
+        try:
+            feats = _backbone_train_forward(m, xs, sd_keep)
+        finally:
+            for b, v in saved or ():
+                b.copy_(v)
         proto, pooled = K.softmax_pool(add_on_logits_hip(m._add_on, feats), pool_mode=0)
         _, out = K.nonneg_linear(pooled, m._classification.weight, m._classification.bias, None)
     return proto, pooled, out

@@ -46,6 +46,9 @@ extern "C" {
 #define PIPNET_EPI_F32_BIAS 10       /* C = A W^T + b, fp32                                            */
 #define PIPNET_EPI_F32_RESID 11      /* C = R + s * (A W^T + b), fp32 C and R (R may alias C)          */
 
+/* ABI version: bumped whenever an exported signature changes.  2: pipnet_wgrad_conv_f32 gained
+ * its `pad` argument (round 2); a caller built against version 1 must not bind this library. */
+#define PIPNET_AMD_ABI_VERSION 2
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
 /* sha256 (hex) of the sources this library was compiled from (build provenance). */

@@ -45,6 +45,8 @@ def _worker(rank, world, port, batch, q):
             # bench.py's call: own shard + every rank's size (no size exchange)
             _, pooled3, out3 = wrapped(xs[start:start + own], inference=True, global_batch=False,
                                        sizes=shard_sizes(batch, world))
+            # gather_proto=True: the whole map on every rank
+            proto4, _, _ = ShardedInference(net, gather_proto=True)(xs, inference=True)
             try:
                 wrapped(xs[start:start + own], inference=True, global_batch=False, sizes=[own + 1] * world)
                 bad_sizes_rejected = False
@@ -52,8 +54,11 @@ def _worker(rank, world, port, batch, q):
                 bad_sizes_rejected = True
         ok = (torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5)
               and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto2.shape[0] == own
-              # DataParallel call pattern: all three outputs cover the whole batch
-              and proto.shape == r_proto.shape and torch.allclose(proto, r_proto, atol=1e-6)
+              # DataParallel call pattern: pooled / logits cover the whole batch everywhere, the
+              # proto map is gathered to rank 0 (DataParallel's output device), shards elsewhere
+              and ((proto.shape == r_proto.shape and torch.allclose(proto, r_proto, atol=1e-6)) if rank == 0
+                   else torch.allclose(proto, r_proto[start:start + own], atol=1e-6))
+              and proto4.shape == r_proto.shape and torch.allclose(proto4, r_proto, atol=1e-6)
               and torch.equal(pooled, pooled3) and torch.equal(out, out3) and bad_sizes_rejected
               and wrapped.module is net)
         q.put((rank, bool(ok)))

@@ -229,7 +229,51 @@ def _c3_bf16(gpu, num_features=0):
     return meta, rec, net, golden_inputs(meta), golden_state_dict(meta), golden_args(meta)
 
 
+# bf16 error budget of the C3 build against the reference's fp32 arithmetic, measured on the
+# golden model (scratch study: oracle bf16 restatement vs oracle fp32 on 16 images of 224x224):
+# pooled |d| <= 0.039, presence flips only within 0.008 of the 0.1 threshold, logits |d| <= 0.156
+# of a 6.2 scale -- but almost all of that is common to every class of an image (the classifier
+# rows are N(1, 0.1), main.py:168, so a pooled error moves every logit alike) -- while the error
+# of the logit *differences* that decide the argmax (d_c - d_top) is <= 0.045, against class
+# margins (top-2 gaps) of 0.07-0.13.  The bounds below sit at about 2x those measurements.
+BF16_POOLED_TOL = 0.06          # present in both: |pooled - pooled_fp32|
+BF16_PRESENCE_BAND = 1e-2       # presence flags must agree where |pooled_fp32 - 0.1| > band
+BF16_MARGIN_TOL = 0.08          # max_c |(out_c - out_top) - (ref_c - ref_top)|, < the median class margin
+BF16_LOGIT_TOL = 0.05           # |out - ref| <= tol * max|ref| (common mode included)
+
+
+def _check_bf16_vs_fp32(pooled, out, r_raw, r_out, min_decisive):
+    """HIP bf16 inference outputs against the reference's fp32 arithmetic (oracle, pinned to
+    the reference goldens): presence flags, pooled values, logits, class-margin error, argmax
+    on every image whose fp32 top-2 gap exceeds the margin bound.  Returns the measured
+    errors so the test log shows the budget actually used."""
+    pooled, out, r_raw, r_out = (t.double() for t in (pooled, out, r_raw, r_out))
+    r_inf = torch.where(r_raw < 0.1, torch.zeros_like(r_raw), r_raw)
+    band = (r_raw - 0.1).abs() <= BF16_PRESENCE_BAND
+    flags_ok = ((pooled > 0) == (r_raw >= 0.1)) | band
+    assert flags_ok.all(), ("presence flag flipped outside the band", r_raw[~flags_ok], pooled[~flags_ok])
+    both = (pooled > 0) & (r_inf > 0)
+    perr = (pooled - r_inf).abs()[both].max().item() if both.any() else 0.0
+    assert perr <= BF16_POOLED_TOL, perr
+    d = out - r_out
+    scale = r_out.abs().max().clamp(min=1.0)
+    assert d.abs().max() <= BF16_LOGIT_TOL * scale, (d.abs().max(), scale)
+    top = r_out.argmax(1)
+    merr = (d - d.gather(1, top[:, None])).abs().max(1).values
+    assert merr.max() <= BF16_MARGIN_TOL, merr
+    srt = r_out.sort(dim=1).values
+    gap = srt[:, -1] - srt[:, -2]
+    decisive = gap > BF16_MARGIN_TOL
+    assert int(decisive.sum()) >= min_decisive, (gap, decisive.sum())
+    assert torch.equal(out.argmax(1)[decisive], top[decisive]), (out.argmax(1), top, gap)
+    return {"pooled_err": perr, "logit_err": d.abs().max().item(), "margin_err": merr.max().item(),
+            "decisive": int(decisive.sum()), "present": int((r_inf > 0).sum()), "band": int(band.sum())}
+
+
 def test_c3_bf16_matches_bf16_oracle_and_reference(gpu):
+    """The golden's 2 images: vs the bf16 restatement of the build's arithmetic and vs the
+    reference's recorded fp32 outputs under the bf16 budget (argmax compared on both images:
+    their fp32 class margins 0.10 / 0.14 exceed BF16_MARGIN_TOL)."""
     from oracle import ref_cpu
     meta, rec, net, xs, sd, args = _c3_bf16(gpu)
     torch.set_num_threads(8)
@@ -244,29 +288,60 @@ def test_c3_bf16_matches_bf16_oracle_and_reference(gpu):
     scale = r_out.abs().max().clamp(min=1.0)
     assert (out - r_out).abs().max() <= 5e-2 * scale
     assert (proto.amax(dim=(2, 3)) - r_proto.amax(dim=(2, 3))).abs().max() <= 5e-2
-    # vs the reference's fp32 outputs (golden): bf16 tolerance
-    g_pooled, g_out = torch.from_numpy(rec["inf_pooled"]), torch.from_numpy(rec["inf_out"])
-    gnear = (g_pooled - 0.1).abs() < 5e-2
-    assert torch.all((pooled - g_pooled).abs()[~gnear] <= 5e-2)
-    gs = g_out.abs().max().clamp(min=1.0)
-    assert (out - g_out).abs().max() <= 5e-2 * gs
-    srt = g_out.sort(dim=1).values
-    decisive = (srt[:, -1] - srt[:, -2]) > 0.1 * gs
-    assert torch.equal(out.argmax(1)[decisive], g_out.argmax(1)[decisive])
+    # vs the reference's fp32 outputs (golden)
+    got = _check_bf16_vs_fp32(pooled, out, torch.from_numpy(rec["raw_pooled"]), torch.from_numpy(rec["inf_out"]),
+                              min_decisive=2)
+    print("C3 golden bf16 budget:", got)
+
+
+def _fp32_oracle_head(xs, sd, args):
+    from oracle import ref_cpu
+    with torch.no_grad():
+        feats = ref_cpu.backbone(xs, sd, args)
+        r_raw = torch.softmax(feats, dim=1).amax(dim=(2, 3))
+        r_out = ref_cpu.non_neg_linear(torch.where(r_raw < 0.1, torch.zeros_like(r_raw), r_raw),
+                                       sd["_classification.weight"], sd.get("_classification.bias"))
+    return r_raw, r_out
+
+
+def test_c3_bf16_16_images_vs_fp32_oracle(gpu):
+    """16 committed-seed images of 224x224 through the HIP bf16 build and the fp32 oracle:
+    presence flags, pooled, logits, class-margin error and argmax under the bf16 budget;
+    at least 8 images must be decisive (the comparison is never empty)."""
+    from count_pipnet_amd.synthetic import synth_images
+    meta, rec, net, _, sd, args = _c3_bf16(gpu)
+    torch.set_num_threads(8)
+    xs = synth_images(16, 224, seed=11)
+    with torch.no_grad():
+        _, pooled, out = net(xs.to(gpu), inference=True)
+    r_raw, r_out = _fp32_oracle_head(xs, sd, args)
+    got = _check_bf16_vs_fp32(pooled.cpu(), out.cpu(), r_raw, r_out, min_decisive=8)
+    print("C3 16-image bf16 budget:", got)
 
 
 def test_c3_bf16_full_batch_properties(gpu):
-    """BASELINE C3 size (bs=128, 224x224): shapes, softmax normalisation, pooled = max of
-    proto, per-image determinism (image 0 alone == image 0 in the batch)."""
+    """BASELINE C3 size (bs=128, 224x224), raw and inference mode: shapes, softmax
+    normalisation, pooled = max of proto (and its 0.1 clamp), logits = NonNegLinear(pooled),
+    per-image determinism (image 0 alone == image 0 in the batch), and 4 images spread over
+    the batch against the fp32 oracle under the bf16 budget."""
     from count_pipnet_amd.synthetic import synth_images
-    meta, rec, net, _, _, _ = _c3_bf16(gpu)
+    meta, rec, net, _, sd, args = _c3_bf16(gpu)
     xs = synth_images(128, 224, seed=11).to(gpu)
     with torch.no_grad():
         proto, pooled, out = net(xs, inference=False)
         p1, pl1, o1 = net(xs[:1], inference=False)
+        _, ipooled, iout = net(xs, inference=True)
     assert tuple(proto.shape) == (128, 2048, 28, 28) and tuple(out.shape) == (128, 200)
     s = proto.sum(dim=1)
     assert torch.allclose(s, torch.ones_like(s), atol=1e-4)
     assert torch.equal(pooled, proto.amax(dim=(2, 3)))
     assert torch.equal(pl1[0], pooled[0]) and torch.equal(o1[0], out[0])
     assert torch.isfinite(out).all()
+    assert torch.equal(ipooled, torch.where(pooled < 0.1, torch.zeros_like(pooled), pooled))
+    w = net._classification.weight
+    assert torch.allclose(iout, ipooled @ torch.relu(w).t(), rtol=1e-5, atol=1e-4)
+    pick = [0, 37, 64, 127]
+    torch.set_num_threads(8)
+    r_raw, r_out = _fp32_oracle_head(xs[pick].cpu(), sd, args)
+    got = _check_bf16_vs_fp32(ipooled[pick].cpu(), iout[pick].cpu(), r_raw, r_out, min_decisive=1)
+    print("C3 bs=128 sample bf16 budget:", got)

@@ -188,7 +188,10 @@ def _ref_grads(rec, pname, upto=None):
     return gs if upto is None else gs[:upto]
 
 
-def _trajectory_close(a, b, grads, lr, what, tally=None):
+RESNET_DECISIVE = 0.25
+
+
+def _trajectory_close(a, b, grads, lr, what, tally=None, decisive=DECISIVE):
     a = a.detach().cpu().double().flatten()
     b = b.detach().cpu().double().flatten()
     n = min([a.numel(), b.numel()] + [g.numel() for g in grads])
@@ -196,7 +199,7 @@ def _trajectory_close(a, b, grads, lr, what, tally=None):
     dec = torch.ones(n, dtype=torch.bool)
     for g in grads:
         g = g.flatten()[:n]
-        dec &= g.abs() > DECISIVE * max(g.abs().max().item(), 1e-30)
+        dec &= g.abs() > decisive * max(g.abs().max().item(), 1e-30)
     steps = len(grads)
     tol = torch.where(dec, TIGHT * lr * steps + 1e-5 * b.abs() + 1e-7,
                       torch.full_like(b, 2.0 * lr * steps * 1.001 + 1e-7))
@@ -226,7 +229,9 @@ def test_finetune_iterations_match_reference(gpu, name):
             _trajectory_close(cls.weight, _t(rec[f"s{i}_w"]), _ref_grads(rec, "_classification.weight", i), lr_max,
                               f"weight before iteration {i}")
         sd_keep = _sd_keep(net, rec[f"s{i}_masks"])
-        proto, pooled, out = T.train_forward_hip(net, torch.cat([xs1, xs2]).to(gpu), sd_keep)
+        # an observer forward: it must not advance a ResNet's BN running statistics (the
+        # training step below does, once, as the reference's forward does)
+        proto, pooled, out = T.train_forward_hip(net, torch.cat([xs1, xs2]).to(gpu), sd_keep, update_bn_stats=False)
         torch.testing.assert_close(pooled.cpu(), _t(rec[f"s{i}_pooled"]), rtol=1e-3, atol=2e-4)
         torch.testing.assert_close(out.cpu(), _t(rec[f"s{i}_out"]), rtol=1e-3, atol=2e-3)
         opt.zero_grad(set_to_none=True)
@@ -254,6 +259,8 @@ def test_finetune_iterations_match_reference(gpu, name):
                           "final bias", tally)
     assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
     assert float(cls.normalization_multiplier[0]) == pytest.approx(float(rec["final_mult"][0]))
+    # ResNet: every BN ran in train mode once per iteration (frozen backbone -> all exact)
+    _check_running_stats(net, rec)
 
 
 def test_train_pipnet_epoch(gpu):
@@ -369,15 +376,15 @@ def test_suffix_training_matches_reference(gpu, name):
     for pname in names:
         p = params[pname].detach().cpu().double()
         head = _t(rec[f"param/{pname}/head"]).double()
-        if resnet:
-            # fp32 ResNet-50 backprop is ~2 % from fp64 for torch as well (see
-            # _resnet_grads_vs_f64), so AdamW's sign-like first steps may differ: every element
-            # within the AdamW step bound (2 lr per iteration), no quorum
-            lr_p = next(g["lr"] for g in opt_net.param_groups if any(q is params[pname] for q in g["params"]))
-            bound = 2.0 * meta["iterations"] * max(lr_p, meta["lr_net"], meta["lr_block"]) * 1.001 + 1e-7
-            assert (p.flatten()[:head.numel()] - head).abs().max().item() <= bound, pname
-            continue
         lr_p = next(g["lr"] for g in opt_net.param_groups if any(q is params[pname] for q in g["params"]))
+        if resnet:
+            # fp32 ResNet-50 backprop is ~2-3 % (of max|g|) from fp64 for torch as well (see
+            # _resnet_grads_vs_f64), so elements with small gradients may take opposite
+            # sign-like AdamW steps (<= 2 lr per iteration); elements whose reference gradient
+            # exceeds RESNET_DECISIVE of max|g| in every iteration -- ~10x that error -- must
+            # follow the reference within TIGHT * lr per step
+            _trajectory_close(p, head, _ref_grads(rec, pname), lr_p, pname, tally, decisive=RESNET_DECISIVE)
+            continue
         _trajectory_close(p, head, _ref_grads(rec, pname), lr_p, pname, tally)
         ref_abs = float(rec[f"param/{pname}/abs"])
         assert float(p.abs().sum()) == pytest.approx(ref_abs, rel=2e-3, abs=1e-3 * p.numel() * lr_max + 1e-6)
@@ -394,6 +401,10 @@ def test_suffix_training_matches_reference(gpu, name):
                           "classifier weight", tally)
     if not resnet:
         assert 3 * tally[0] >= tally[1], tally           # not vacuous: >= 1/3 of the elements decisive
+    else:
+        assert 20 * tally[0] >= tally[1], tally          # >= 5 % of the ResNet elements held tightly
+    if resnet:
+        _check_running_stats_trainable(net, rec, iters)
 
 
 def _check_running_stats(net, rec):
@@ -421,6 +432,35 @@ def _check_running_stats(net, rec):
     for k in rec:
         if k.startswith("buffer/") and k.endswith("num_batches_tracked"):
             assert int(bufs[k[len("buffer/"):]]) == int(rec[k]), k
+
+
+def _check_running_stats_trainable(net, rec, iters):
+    """Running statistics of the BNs in and after the first trainable block.  Iteration 1's
+    batch statistics see the initial weights (as exact as the frozen prefix); the later ones
+    see weights that AdamW moved by sign-like steps where fp32 backprop differs, so each such
+    BN is held to the reference within the momentum-weighted share of those iterations:
+    |rm - rm_ref| <= 1e-3 + 0.1 * (iters - 1) * 5e-2 * max|rm_ref| (momentum 0.1, batch
+    statistics within 5 % of their scale).  Prints the worst relative deviation seen."""
+    from count_pipnet_amd import resnet_train as R
+    start = R.trainable_start(net._net)
+    keys = [f"_net.{k}." for k, _ in R._blocks(net._net)[start:]]
+    bufs = dict(net.named_buffers())
+    worst, checked = 0.0, 0
+    for k in rec:
+        if not (k.startswith("buffer/") and k.endswith("/head")):
+            continue
+        bname = k[len("buffer/"):-len("/head")]
+        if not bname.startswith(tuple(keys)) or not bname.endswith(("running_mean", "running_var")):
+            continue
+        b = bufs[bname].detach().cpu().double().flatten()
+        head = _t(rec[k]).double()
+        scale = head.abs().max().item()
+        dev = (b[:head.numel()] - head).abs().max().item()
+        worst = max(worst, dev / max(scale, 1e-12))
+        assert dev <= 1e-3 + 0.1 * (iters - 1) * 5e-2 * scale, (bname, dev, scale)
+        checked += 1
+    assert checked >= 2
+    print(f"trainable-block BN running statistics: {checked} checked, worst deviation {worst:.3g} of scale")
 
 
 def _torch_path_grads(net, xs, ys, masks_in_order, w_align, w_tanh, w_class, mult):
