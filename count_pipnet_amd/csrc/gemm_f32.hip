@@ -82,6 +82,21 @@ bool gemm_persist() {
   return g_gemm_persist == 1;
 }
 
+// PIPNET_GEMM_STREAM=0/1 (read once; default 0 -- measured 3-5 % slower than the regular tile, profiles/r03/gemm_stream_ab.txt): the streaming persistent tile with deferred
+// epilogues (gemm_f32_tn_stream_kernel) for variant-3 dense GEMMs with N % 128 == 0, K >= 256
+// and at least two tiles per workgroup slot.
+#ifndef PIPNET_GEMM_STREAM_DEFAULT
+#define PIPNET_GEMM_STREAM_DEFAULT 0
+#endif
+int g_gemm_stream = -1;
+bool gemm_stream() {
+  if (g_gemm_stream < 0) {
+    const char* e = getenv("PIPNET_GEMM_STREAM");
+    g_gemm_stream = e ? (e[0] == '1') : PIPNET_GEMM_STREAM_DEFAULT;
+  }
+  return g_gemm_stream == 1;
+}
+
 template <int ALOAD>
 int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   p.nt = (p.N + BN - 1) / BN;
@@ -93,6 +108,28 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   const int v = gemm_variant(p.M, p.N, p.K, vec);
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
+  if (ALOAD == ALOAD_DENSE && v == 3 && p.vec_epi && p.N % BN == 0 && p.K % 32 == 0 && p.K >= 256 &&
+      epi != PIPNET_EPI_RESID_ROWSCALE && p.mt * p.nt >= 4 * num_cus() && (int64_t)p.M * p.lda < (1LL << 31) &&
+      (int64_t)p.N * p.K < (1LL << 31) && (int64_t)p.M * p.ldc < (1LL << 31) &&
+      (!p.R || (int64_t)p.M * p.ldr < (1LL << 31)) && gemm_stream()) {
+    const dim3 sgrid(2 * num_cus());
+#define PIPNET_STREAM_CASE(E) \
+  case E: hipLaunchKernelGGL((gemm_f32_tn_stream_kernel<E>), sgrid, block, 0, s, p); break;
+    switch (epi) {
+      PIPNET_STREAM_CASE(PIPNET_EPI_NONE)
+      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS)
+      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_GELU)
+      PIPNET_STREAM_CASE(PIPNET_EPI_RESID)
+      PIPNET_STREAM_CASE(PIPNET_EPI_MUL)
+      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_RELU)
+      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_RESID_RELU)
+      PIPNET_STREAM_CASE(PIPNET_EPI_GELU_BWD)
+      default: return PIPNET_ERR_ARG;
+    }
+#undef PIPNET_STREAM_CASE
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   if (ALOAD == ALOAD_DENSE && v == 3 && p.vec_epi && p.N % BN == 0 && gemm_persist()) {
     const int ntiles = p.mt * p.nt;
     const dim3 pgrid(ntiles < 2 * num_cus() ? ntiles : 2 * num_cus());
@@ -146,6 +183,12 @@ extern "C" int pipnet_gemm_persist(int mode) {
   if (mode == 0 || mode == 1) g_gemm_persist = mode;
   else if (mode != -1) return PIPNET_ERR_ARG;
   return gemm_persist() ? 1 : 0;
+}
+
+extern "C" int pipnet_gemm_stream(int mode) {
+  if (mode == 0 || mode == 1) g_gemm_stream = mode;
+  else if (mode != -1) return PIPNET_ERR_ARG;
+  return gemm_stream() ? 1 : 0;
 }
 
 extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,

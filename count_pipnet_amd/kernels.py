@@ -44,9 +44,32 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     if n <= 384 or k <= 192 or m <= 64:
         npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
+    if aload == 0 and n % 128 == 0 and k >= 256 and epilogue != _lib.EPI_RESID_ROWSCALE \
+            and -(-m // 128) * (n // 128) >= 4 * _num_cus() and gemm_stream():
+        return f"pipnet_gemm::gemm_f32_tn_stream_kernel<{epilogue}>"
     if aload == 0 and n % 128 == 0 and gemm_persist():
         return f"pipnet_gemm::gemm_f32_tn_persist_kernel<{epilogue}>"
     return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
+
+
+_CUS = None
+
+
+def _num_cus() -> int:
+    global _CUS
+    if _CUS is None:
+        _CUS = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
+            if torch.cuda.is_available() else 256
+    return _CUS
+
+
+def gemm_stream(mode: int = -1) -> bool:
+    """The library's streaming-GEMM switch (include/pipnet_amd.h pipnet_gemm_stream): mode 1 / 0
+    sets it, -1 queries."""
+    r = _lib.load().pipnet_gemm_stream(mode)
+    if r < 0:
+        _lib.check(r, f"pipnet_gemm_stream({mode})")
+    return bool(r)
 
 
 def gemm_persist(mode: int = -1) -> bool:

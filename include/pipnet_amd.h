@@ -71,6 +71,15 @@ int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* 
  * negative status.  Not thread-safe against concurrent launches (process-wide A/B switch). */
 int pipnet_gemm_persist(int mode);
 
+/* Streaming persistent 128x128 fp32 GEMM tile (stage-3/4 CNBlock Linears: N % 128 == 0,
+ * K % 32 == 0, K >= 256, >= 4 tiles per CU): two workgroups per CU walk their tiles as one
+ * stream of K-tiles and each tile's epilogue runs sliced under the next tile's main loop.
+ * Bitwise equal to the regular tile.  mode 1 on, 0 off, -1 query only; returns the mode in
+ * force (initially PIPNET_GEMM_STREAM from the environment, else off: 3-5 % slower than the
+ * regular tile on the stage-3/4 shapes, profiles/r03/gemm_stream_ab.txt) or a negative status.
+ * Takes precedence over pipnet_gemm_persist.  Process-wide A/B switch. */
+int pipnet_gemm_stream(int mode);
+
 /* pipnet_linear_f32 with PIPNET_EPI_RESID_ROWSCALE: C = R + row_scale[m / rows_per_scale] *
  * (scale * (A W^T + bias)).  The CNBlock's Linear2 * layer_scale + residual under
  * torchvision's StochasticDepth("row") in train mode: rows_per_scale = H*W (one factor per

@@ -357,3 +357,56 @@ def test_gemm_persistent_bitwise(gpu, m, n, k, epi):
     elif epi == "resid":
         ref = r.double() + s.double() * (ref + b.double())
     assert (outs[1].double() - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("m,n,k,epi", [
+    (46656 // 2, 1536, 384, "gelu"),     # stage-3 fc1 shape (half batch): many tiles per workgroup
+    (46656, 1536, 384, "gelu"),          # stage-3 fc1, full C2 batch
+    (20001, 3072, 768, "gelu"),          # stage-4 fc1 shape, ragged M (last tile 33 rows)
+    (43264, 768, 3072, "resid"),         # stage-4 fc2: residual epilogue, K = 3072
+    (30000, 1024, 256, "none"),          # K = 256: exactly 8 K-tiles per tile (one slice each)
+    (30001, 1024, 512, "bias"),          # bias epilogue, ragged M
+])
+def test_gemm_stream_bitwise(gpu, m, n, k, epi):
+    """The streaming tile (pipnet_gemm_stream: K-tiles of consecutive tiles as one DMA stream,
+    each tile's epilogue sliced under the next tile's main loop, stores from the MFMA layout)
+    against the regular 128x128 tile: bitwise equal, rows past M never written, and within
+    1e-3 of an fp64 reference.  The residual case runs in place (R aliases C, as the CNBlock
+    residual stream does)."""
+    g = torch.Generator().manual_seed(m + n + k)
+    a = torch.randn(m, k, generator=g).to(gpu)
+    w = (torch.randn(n, k, generator=g) * 0.05).to(gpu)
+    b = torch.randn(n, generator=g).to(gpu)
+    s = torch.randn(n, generator=g).to(gpu)
+    r = torch.randn(m, n, generator=g).to(gpu)
+    e = {"gelu": _lib.EPI_BIAS_GELU, "resid": _lib.EPI_RESID, "none": _lib.EPI_NONE, "bias": _lib.EPI_BIAS}[epi]
+    prev = K.gemm_stream()
+    try:
+        outs = []
+        for mode in (0, 1):
+            K.gemm_stream(mode)
+            assert ("stream" in K.gemm_kernel_name(m, n, k, e, 0)) == bool(mode)
+            if epi == "resid":
+                buf = torch.empty(m + 7, n, device=gpu)
+                buf[m:] = 12345.0                                   # rows past M: must stay untouched
+                buf[:m] = r
+                K.linear(a, w, b, e, scale=s, r=buf[:m], out=buf[:m])
+                outs.append(buf)
+            else:
+                buf = torch.full((m + 7, n), 12345.0, device=gpu)
+                K.linear(a, w, b, e, scale=s, out=buf[:m])
+                outs.append(buf)
+        torch.cuda.synchronize()
+    finally:
+        K.gemm_stream(int(prev))
+    diff = (outs[0] - outs[1]).abs()
+    assert torch.equal(outs[0], outs[1]), (int((diff > 0).sum()), float(diff.max()), (diff > 0).nonzero()[:4].tolist())
+    assert torch.all(outs[1][m:] == 12345.0)
+    ref = a.double() @ w.double().t()
+    if epi == "gelu":
+        ref = torch.nn.functional.gelu(ref + b.double())
+    elif epi == "resid":
+        ref = r.double() + s.double() * (ref + b.double())
+    elif epi == "bias":
+        ref = ref + b.double()
+    assert (outs[1][:m].double() - ref).abs().max().item() < 1e-3
