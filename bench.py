@@ -285,21 +285,24 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def timed(model, inp, batch, steps, warmup):
-        """W warm-up steps, then K steps bracketed by barrier + synchronize; every MFMA GEMM /
-        conv launch in the timed region is bracketed by HIP events on the stream it is launched
-        on (torch's current stream) for the dominant-kernel roofline.  Max over ranks."""
+    def timed(model, inp, batch, steps, warmup, instrument=False):
+        """W warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
+        ``instrument``: every MFMA GEMM / conv launch in the timed region is bracketed by HIP
+        events on the stream it is launched on (torch's current stream) for the
+        dominant-kernel roofline -- a separate pass, so the events' own cost never enters
+        ``value``."""
         def step():
             with torch.no_grad():
                 model(inp, inference=True, global_batch=False, sizes=[batch] * world)
         for _ in range(warmup):
             step()
         timer = GemmTimer()
-        kernels.set_launch_hook(timer)
+        if instrument:
+            kernels.set_launch_hook(timer)
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
-        timer.enabled = True
+        timer.enabled = instrument
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
@@ -328,9 +331,25 @@ def main():
         # is the bf16 dense peak / 3 (achieved counts the algorithmic 2*M*N*K fp32 flops)
         return lambda dom: PEAK_BF16_TFLOPS / 3.0 if split and "bf16" in dom else PEAK_F32_TFLOPS
 
-    elapsed, agg = timed(sharded, xs, a.batch, a.steps, a.warmup)
+    from count_pipnet_amd.pipnet import set_stream_split, stream_split
+
+    def measure(model, inner, inp, batch, steps, peak_of):
+        """Throughput with the model's default stream split (clean pass), then the roofline
+        pass: one stream (per-kernel events must not overlap another stream's kernels),
+        instrumented.  Returns (elapsed, roofline dict, agg, extra fields)."""
+        nsplit = stream_split(inner, inp)
+        el, _ = timed(model, inp, batch, steps, a.warmup)
+        set_stream_split(inner, 1)
+        el1, agg = timed(model, inp, batch, steps, max(1, a.warmup // 2), instrument=True)
+        set_stream_split(inner, nsplit)
+        _, roof = roofline(agg, steps, peak_of)
+        info = {"stream_split": nsplit, "roofline_pass": {"streams": 1, "instrumented": True,
+                                                          "ms_per_step": el1 / steps * 1e3}}
+        return el, roof, agg, info
+
     split = a.precision == "bf16x3"
-    dom, roof = roofline(agg, a.steps, peak_for(split))
+    elapsed, roof, agg, info = measure(sharded, net, xs, a.batch, a.steps, peak_for(split))
+    dom = roof["kernel"]
     gemm_flops = sum(v[1] for v in agg.values())
     gemm_time = sum(v[2] for v in agg.values())
     imgs = a.batch * world * a.steps
@@ -359,15 +378,16 @@ def main():
         "roofline": roof,
         "model_tflops": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3,
         "model_frac_of_f32_peak": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,
-        "gemm_all": {"tflops": gemm_flops / gemm_time / 1e12, "ms_per_step": gemm_time / a.steps * 1e3},
+        "gemm_all": {"tflops": gemm_flops / gemm_time / 1e12,
+                     "ms_per_step": gemm_time / a.steps * 1e3, "pass": "roofline pass (one stream)"},
     }
+    result.update(info)
     result["roofline"]["traffic"], result["roofline"]["traffic_source"] = measured_traffic(dom)
     if a.alt_precision != "none" and a.alt_precision != a.precision:
         # the same network and inputs with the other GEMM precision, timed the same way
         from count_pipnet_amd.pipnet import set_hip_dtype
         set_hip_dtype(net, a.alt_precision)
-        el2, agg2 = timed(sharded, xs, a.batch, a.steps, a.warmup)
-        _, roof2 = roofline(agg2, a.steps, peak_for(a.alt_precision == "bf16x3"))
+        el2, roof2, _, info2 = measure(sharded, net, xs, a.batch, a.steps, peak_for(a.alt_precision == "bf16x3"))
         ms2 = el2 / a.steps * 1e3
         result["alt_precision"] = {
             "precision": a.alt_precision,
@@ -377,35 +397,26 @@ def main():
             "accuracy": "fp32 inputs/outputs and accumulation; products of hi+lo bf16 splits (~1e-5 relative "
                         "per product); parity vs the reference goldens at the north-star 1e-3 "
                         "(tests/test_gpu_parity.py::test_hip_bf16x3_*)" if a.alt_precision == "bf16x3" else "exact"}
+        result["alt_precision"].update(info2)
     del sharded, net, xs
     torch.cuda.empty_cache()
 
     if not a.no_extra:
-        from count_pipnet_amd.pipnet import set_stream_split, stream_split
         extra = {}
         for name, cfg in EXTRA.items():
             enet = make_extra(cfg, dev)
             ewrap = ShardedInference(enet)
             exs = synth_images(cfg["batch"], cfg["size"], seed=200 + rank).to(dev)
-            # throughput with the model's default stream split (C3: two half-batch streams)
-            nsplit = stream_split(enet, exs) if hasattr(enet, "_hip_logits") else 1
             esteps = max(a.steps, 10)
-            el, eagg = timed(ewrap, exs, cfg["batch"], esteps, a.warmup)
+            el, eroof, _, einfo = measure(ewrap, enet, exs, cfg["batch"], esteps, lambda dom, p=cfg["peak"]: p)
             rec = {"baseline": cfg["baseline"], "workload": cfg["workload"], "dtype": cfg["dtype"],
                    "per_gpu_batch": cfg["batch"], "global_batch": cfg["batch"] * world, "image_size": cfg["size"],
                    "value": cfg["batch"] * world * esteps / el, "unit": "images/sec",
-                   "ms_per_step": el / esteps * 1e3, "steps": esteps, "stream_split": nsplit,
+                   "ms_per_step": el / esteps * 1e3, "steps": esteps,
                    "model_tflops": cfg["gflop"] * cfg["batch"] / (el / esteps) / 1e3,
-                   "model_frac_of_peak": cfg["gflop"] * cfg["batch"] / (el / esteps) / 1e3 / cfg["peak"]}
-            if nsplit > 1:
-                # per-kernel durations of co-running streams overlap: the roofline comes from a
-                # one-stream pass over the same inputs
-                set_stream_split(enet, 1)
-                el1, eagg = timed(ewrap, exs, cfg["batch"], esteps, a.warmup)
-                set_stream_split(enet, nsplit)
-                rec["one_stream_ms_per_step"] = el1 / esteps * 1e3
-                rec["roofline_pass"] = "one stream (per-kernel events do not overlap another stream's kernels)"
-            _, rec["roofline"] = roofline(eagg, esteps, lambda dom, p=cfg["peak"]: p)
+                   "model_frac_of_peak": cfg["gflop"] * cfg["batch"] / (el / esteps) / 1e3 / cfg["peak"],
+                   "roofline": eroof}
+            rec.update(einfo)
             extra[name] = rec
             del ewrap, enet, exs
             torch.cuda.empty_cache()

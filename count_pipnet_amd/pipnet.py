@@ -122,10 +122,11 @@ class PIPNet(nn.Module):
 # Concurrent sub-batches: batches of at least STREAM_SPLIT_MIN_BATCH images run as n
 # half-batch forwards on n HIP streams, so one half's tile-quantisation tails and
 # bandwidth-bound kernels co-run with the other half's MFMA tiles.  Default 2 for ResNet
-# backbones (C3 bs=128: bf16 15.3k -> 17.2k img/s, fp32 +3 %, profiles/r02/stream_split_c3.log;
-# 3 streams equal, 4 no gain), 1 for ConvNeXt, where it is opt-in (set_stream_split(net, 2):
-# +2.5 % on BASELINE C2) so bench.py's per-kernel roofline timings describe one launch, not
-# two co-running ones.
+# backbones (C3 bs=128: bf16 17.8k -> 20.1-20.3k img/s; 3 streams 19.6k) and for the full
+# ConvNeXt PIP-Net (C2 bs=64: 2,933 -> 2,974-2,977 img/s; 3 streams 2,954-2,964), 1 for
+# CountPIPNet / mid-layer backbones (C5 64 images: 55.8-56.1k -> 51.4-51.8k with 2 streams)
+# -- profiles/r03/stream_split_ab.txt.  bench.py takes per-kernel roofline timings from a
+# separate one-stream pass, where each launch runs alone.
 STREAM_SPLIT_MIN_BATCH = 32
 _SIDE_STREAMS = {}
 
@@ -139,7 +140,7 @@ def _side_streams(dev, n):
 
 def set_stream_split(net: nn.Module, n: int) -> nn.Module:
     """Number of concurrent sub-batch streams for the HIP forward (1 = off; default 2 for
-    ResNet backbones, 1 otherwise).  Outputs are bit-identical either way (every kernel is
+    ResNet and full ConvNeXt PIP-Net backbones, 1 otherwise).  Outputs are bit-identical either way (every kernel is
     batch-invariant)."""
     (net.module if hasattr(net, "module") else net)._hip_stream_split = int(n)
     return net
@@ -148,8 +149,11 @@ def set_stream_split(net: nn.Module, n: int) -> nn.Module:
 def stream_split(model: nn.Module, xs: Tensor) -> int:
     n = getattr(model, "_hip_stream_split", None)
     if n is None:
+        from .convnext_features import ConvNeXt
         from .resnet_features import ResNet_features
-        n = 2 if isinstance(getattr(model, "_net", None), ResNet_features) else 1
+        net = getattr(model, "_net", None)
+        full_convnext = isinstance(net, ConvNeXt) and not hasattr(model, "_max_count")
+        n = 2 if isinstance(net, ResNet_features) or full_convnext else 1
     if n <= 1 or xs.shape[0] < max(STREAM_SPLIT_MIN_BATCH, n):
         return 1
     return n

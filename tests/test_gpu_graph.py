@@ -111,6 +111,24 @@ def test_stream_split_resnet_default(gpu, dtype):
         assert torch.equal(a, b)
 
 
+def test_stream_split_convnext_default(gpu):
+    """The full ConvNeXt PIP-Net (C2's model) splits batches >= 32 over 2 streams by default;
+    bit-identical to the one-stream forward.  CountPIPNet / mid-layer models stay on one."""
+    from count_pipnet_amd.pipnet import set_stream_split, stream_split
+    from count_pipnet_amd.synthetic import synth_images
+    net, _, _ = _net("c2_pipnet_convnext26", gpu)
+    xs = synth_images(34, 64, seed=12).to(gpu)
+    assert stream_split(net, xs) == 2 and stream_split(net, xs[:16]) == 1
+    with torch.no_grad():
+        split = [t.clone() for t in net(xs, inference=True)]
+        set_stream_split(net, 1)
+        one = [t.clone() for t in net(xs, inference=True)]
+    for a, b in zip(split, one):
+        assert torch.equal(a, b)
+    cnet, _, _ = _net("c5_count_bilinear_2048", gpu)
+    assert stream_split(cnet, synth_images(40, 32, seed=1)) == 1
+
+
 @pytest.mark.parametrize("noise", ["injected", "philox"])
 def test_count_stream_split_bit_identical(gpu, noise):
     """CountPIPNet split forward (backbone + Gumbel head per sub-batch stream, count layers on

@@ -189,11 +189,16 @@ def _ref_grads(rec, pname, upto=None):
 
 
 # ResNet-50: decisive = |g| > 25 % of max|g| in every iteration with one sign throughout; held
-# to half a sign-like step per iteration (4x tighter than the generic bound).  Iteration 2's
-# gradients already see weights that iteration 1 moved by opposite sign-like steps wherever fp32
-# backprop differs (small-gradient elements), so the decisive elements drift by up to ~0.5 lr
-# (measured: <= 2.4e-4 at lr 5e-4 after 2 iterations) -- more than TIGHT allows.
-RESNET_DECISIVE, RESNET_TIGHT = 0.25, 0.5
+# to one lr per iteration (half the generic 2 lr; a wrong-sign update in every iteration would
+# differ by ~2 lr per iteration).  Iteration 2's gradients already see weights that iteration 1
+# moved by opposite sign-like steps wherever fp32 backprop differs (small-gradient elements,
+# and everything downstream of them), so decisive elements drift by up to ~0.65 lr per
+# iteration (measured, lr 5e-4, 2 iterations) -- more than TIGHT allows.
+RESNET_DECISIVE, RESNET_TIGHT = 0.25, 1.0
+# The generic bound: AdamW's step is lr * m_hat / (sqrt(v_hat) + eps), and at iteration 2
+# m_hat / sqrt(v_hat) peaks at 1.00136 (g2 = 1.11 g1); two trajectories stepping in opposite
+# directions differ by <= 2 * 1.00136 lr per iteration, hence the 1.005 factor.
+STEP_BOUND = 1.005
 
 
 def _trajectory_close(a, b, grads, lr, what, tally=None, decisive=DECISIVE, same_sign=False, tight=TIGHT):
@@ -214,7 +219,7 @@ def _trajectory_close(a, b, grads, lr, what, tally=None, decisive=DECISIVE, same
             dec &= g.flatten()[:n].sign() == s0
     steps = len(grads)
     tol = torch.where(dec, tight * lr * steps + 1e-5 * b.abs() + 1e-7,
-                      torch.full_like(b, 2.0 * lr * steps * 1.001 + 1e-7))
+                      torch.full_like(b, 2.0 * lr * steps * STEP_BOUND + 1e-7))
     d = (a - b).abs()
     bad = d > tol
     assert not bool(bad.any()), (f"{what}: {int(bad.sum())} / {n} elements beyond the AdamW step tolerance "
@@ -407,7 +412,7 @@ def test_suffix_training_matches_reference(gpu, name):
         # iteration 2's classifier gradient sees the backbone after one AdamW step whose
         # sign-like updates differ where fp32 backprop does (see above): AdamW step bound
         w8 = _t(rec["final_w_rows8"]).double()
-        assert (cls.weight[:8].detach().cpu().double() - w8).abs().max().item() <= 2 * meta["lr"] * iters * 1.001
+        assert (cls.weight[:8].detach().cpu().double() - w8).abs().max().item() <= 2 * meta["lr"] * iters * STEP_BOUND
     elif not pretrain:
         w = _t(rec["final_w"]) if "final_w" in rec else _t(rec["final_w_rows8"])
         _trajectory_close(cls.weight[:w.shape[0]], w, _ref_grads(rec, "_classification.weight"), meta["lr"],

@@ -1,6 +1,7 @@
 """Throughput of the non-headline BASELINE configs on one GPU (bench.py measures configs[1]).
 
   C1  CountPIPNet identity.yaml, 64x64, bs=16          (the reference's CPU case; here on HIP)
+  C2  PIP-Net ConvNeXt-tiny-26 224x224, bs=64, fp32     (bench.py's headline, for stream-split A/B)
   C3  PIP-Net ResNet50 224x224, bs=128, bf16 (BASELINE C3) and fp32 (exact reference arithmetic)
   C5  CountPIPNet bilinear 2048 prototypes, 128x128, 64 images per GPU (bs=256 over 4 GPUs)
   C2' PIP-Net ConvNeXt-tiny-13 224x224, bs=64          (the 13x13 variant)
@@ -35,6 +36,8 @@ CONFIGS = {
                args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=16,
                          activation="gumbel_softmax", intermediate_layer="identity", max_count=3, use_ste=True,
                          bias=False), gflop=0.2495),
+    "c2": dict(model="pipnet", batch=64, size=224, classes=200,
+               args=dict(net="convnext_tiny_26", num_features=0, bias=False), gflop=40.094),
     "c3": dict(model="pipnet", batch=128, size=224, classes=200, args=dict(net="resnet50", num_features=0, bias=False,
                                                                            hip_dtype="bf16"), gflop=38.16),
     "c3_fp32": dict(model="pipnet", batch=128, size=224, classes=200,
@@ -47,7 +50,7 @@ CONFIGS = {
                   args=dict(net="convnext_tiny_13", num_features=0, bias=False), gflop=12.617),
 }
 # the split-bf16 build of every ConvNeXt config (fp32 in / out, three bf16 products per fp32 product)
-for _k in ("c1", "c5", "c2_13"):
+for _k in ("c1", "c2", "c5", "c2_13"):
     CONFIGS[_k + "_bf16x3"] = dict(CONFIGS[_k], args=dict(CONFIGS[_k]["args"], hip_dtype="bf16x3"))
 
 
