@@ -57,136 +57,6 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// ======================================================================================
-// Skinny GEMM (M <= 64 rows, e.g. C5's BilinearIntermediate at M = batch): the weights W
-// [N][K] are read exactly once, so nothing is gained by staging them through LDS.  Every wave
-// streams its own 64 columns of W and the (L1/L2-resident) A rows straight into registers
-// with float4 loads and multiplies on v_mfma_f32_32x32x2_f32: with the k-slot permutation of
-// gemm_f32_impl.hpp (lane (row|col, h = l >> 5) supplies k = 16 h + j in MFMA j of a 32-deep
-// step) a lane's 16 k-values of a row are 64 contiguous bytes of that row, for A and W alike.
-// A workgroup = 4 waves on the same 64 columns, each wave one quarter of the workgroup's K
-// slab; the quarters are summed through LDS in wave order, and the slab partial goes to the
-// split-K workspace, which splitk_reduce_kernel sums in slab order with the epilogue.  No
-// barrier in the main loop; loads of step t+1 are in flight under the MFMAs of step t.
-// At M = 64 an fp32 weight element feeds 2 x 64 flops: 32 flop / byte, above the fp32-MFMA
-// ridge (157 TF/s / 8 TB/s = 20), so the bound is the MFMA pipe, not HBM.
-// The per-row result depends on (N, K) only -- the slab split is chosen from them -- never
-// on M (rows past M are clamped loads, never stored).
-// ======================================================================================
-template <int RB>
-__global__ __launch_bounds__(256, 2) void skinny_gemm_kernel(const float* __restrict__ A, int64_t lda,
-                                                           const float* __restrict__ W, int M, int N, int K,
-                                                           int kslab, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) float red[3 * 64 * RB * 2 * 16];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 64;
-  const int kq = kslab / 4;                                   // per-wave K range (multiple of 32)
-  const int kb = blockIdx.y * kslab + wid * kq;
-  const int ke = min(kb + kq, K);
-  const float* arow[RB];
-  const float* wrow[2];
-#pragma unroll
-  for (int i = 0; i < RB; ++i) arow[i] = A + (int64_t)min(32 * i + r, M - 1) * lda + 16 * h;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) wrow[j] = W + (int64_t)(n0 + 32 * j + r) * K + 16 * h;
-  f32x16 acc[RB][2];
-#pragma unroll
-  for (int i = 0; i < RB; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
-  // One register set of operands: slice q (k = 16 h + 4 q .. + 3 of the step) is reloaded for
-  // the next step right after its 4 x RB x 2 MFMAs, a whole step ahead of its use.  The loads
-  // are inline asm with explicit waits: hipcc's own wait counting drains every load at the top
-  // of the loop (vmcnt(0)), which would expose the full memory latency once per step.  Issue
-  // order per step: [mma q, load q] for q = 0..3, so before mma q exactly 3 slices of loads
-  // (3 (2 + RB) instructions) are younger than the ones it needs -- in every step, since the
-  // last step re-loads its own operands (unused) to keep the pattern.  The wait names the
-  // slice's registers as in/out operands, so no MFMA can be scheduled above it.
-  constexpr int LPS = 2 + RB;                                 // loads per slice
-  f32x4 a[RB][4], w[2][4];
-  auto gload = [](f32x4& d, const float* p) {
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(d) : "v"(p) : "memory");
-  };
-  auto load_q = [&](int q, int k) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j) gload(w[j][q], wrow[j] + k + 4 * q);
-#pragma unroll
-    for (int i = 0; i < RB; ++i) gload(a[i][q], arow[i] + k + 4 * q);
-  };
-  auto wait_q = [&](int q) {
-    if constexpr (RB == 2)
-      asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0][q]), "+v"(w[1][q]), "+v"(a[0][q]), "+v"(a[1][q]) : "n"(3 * LPS));
-    else
-      asm volatile("s_waitcnt vmcnt(%3)" : "+v"(w[0][q]), "+v"(w[1][q]), "+v"(a[0][q]) : "n"(3 * LPS));
-  };
-  auto mma_q = [&](int q) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][q][e], w[j][q][e], acc[i][j], 0, 0, 0);
-  };
-  if (kb < ke) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) load_q(q, kb);
-    for (int k = kb; k < ke; k += 32) {
-      const int kn = k + 32 < ke ? k + 32 : k;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        wait_q(q);
-        mma_q(q);
-        load_q(q, kn);
-      }
-    }
-    // the trailing re-loads must land before their registers are reused
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if constexpr (RB == 2)
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[0][q]), "+v"(w[1][q]), "+v"(a[0][q]), "+v"(a[1][q]));
-      else
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[0][q]), "+v"(w[1][q]), "+v"(a[0][q]));
-    }
-  }
-  // quarter sums in wave order: waves 1..3 park their accumulators, wave 0 adds them
-  constexpr int PER = RB * 2 * 16;
-  if (wid > 0) {
-    float* dst = red + (wid - 1) * 64 * PER;
-#pragma unroll
-    for (int i = 0; i < RB; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) dst[((i * 2 + j) * 16 + v) * 64 + lane] = acc[i][j][v];
-  }
-  __syncthreads();
-  if (wid != 0) return;
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    const float* src = red + w * 64 * PER;
-#pragma unroll
-    for (int i = 0; i < RB; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) acc[i][j][v] += src[((i * 2 + j) * 16 + v) * 64 + lane];
-  }
-  float* out = ws + (int64_t)blockIdx.y * M * N;
-#pragma unroll
-  for (int i = 0; i < RB; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) {
-        const int m = 32 * i + (v & 3) + 8 * (v >> 2) + 4 * h;
-        if (m < M) out[(int64_t)m * N + n0 + 32 * j + r] = acc[i][j][v];
-      }
-}
-
 // compute units of the current device, queried once
 int num_cus() {
   static int n = 0;
@@ -398,69 +268,6 @@ extern "C" int pipnet_conv2d_nhwc_f32(const float* x, int B, int H, int W, int C
     return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
   }
   return launch_gemm<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
-}
-
-// K slab per workgroup of the skinny GEMM (4 waves x a multiple of 32), from (N, K) only:
-// about 2 workgroups per CU (each wave >= 2 K-steps).
-static int skinny_kslab(int N, int K) {
-  const int nb = N / 64;
-  int slabs = (2 * num_cus() + nb - 1) / nb;
-  int kslab = (K + slabs - 1) / slabs;
-  kslab = (kslab + 127) / 128 * 128;
-  return kslab < 256 ? 256 : kslab;
-}
-
-extern "C" int pipnet_skinny_splits(int N, int K) {
-  if (N <= 0 || K <= 0) return PIPNET_ERR_ARG;
-  const int ks = skinny_kslab(N, K);
-  return (K + ks - 1) / ks;
-}
-
-extern "C" int pipnet_linear_skinny_f32(const float* A, int64_t lda, const float* W, const float* bias,
-                                        const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
-                                        int M, int N, int K, int epilogue, float* workspace, void* stream) {
-  if (M < 0 || M > 64 || N <= 0 || K <= 0 || (N % 64) || (K % 32) || (lda & 3) || lda < K || (ldc & 3) || ldc < N)
-    return PIPNET_ERR_ARG;
-  if (!workspace || !A || !W || !C) return PIPNET_ERR_ARG;
-  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_GELU_BWD || epilogue == PIPNET_EPI_RESID_ROWSCALE)
-    return PIPNET_ERR_ARG;
-  if ((epilogue == PIPNET_EPI_RESID || epilogue == PIPNET_EPI_MUL || epilogue == PIPNET_EPI_BIAS_RESID_RELU ||
-       epilogue == PIPNET_EPI_GELU_BWD) &&
-      (!R || ldr < N || (ldr & 3) || !aligned16(R)))
-    return PIPNET_ERR_ARG;
-  if (!aligned16(A) || !aligned16(W) || !aligned16(C) || !aligned16(workspace) || (bias && !aligned16(bias)) ||
-      (scale && !aligned16(scale)))
-    return PIPNET_ERR_ALIGN;
-  if (M == 0) return PIPNET_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const int kslab = skinny_kslab(N, K);
-  const int splits = (K + kslab - 1) / kslab;
-  const dim3 grid(N / 64, splits);
-  if (M > 32) hipLaunchKernelGGL((skinny_gemm_kernel<2>), grid, dim3(256), 0, s, A, lda, W, M, N, K, kslab, workspace);
-  else hipLaunchKernelGGL((skinny_gemm_kernel<1>), grid, dim3(256), 0, s, A, lda, W, M, N, K, kslab, workspace);
-  PIPNET_CHECK_LAUNCH();
-  const int64_t work = (int64_t)M * (N / 4);
-  const int blocks = (int)((work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096);
-  const int64_t slab = (int64_t)M * N;
-#define PIPNET_RED(E)                                                                                      \
-  case E:                                                                                                 \
-    hipLaunchKernelGGL((splitk_reduce_kernel<E>), dim3(blocks), dim3(256), 0, s, workspace, splits, slab, M, N, \
-                       bias, scale, R, ldr, C, ldc);                                                      \
-    break;
-  switch (epilogue) {
-    PIPNET_RED(PIPNET_EPI_NONE)
-    PIPNET_RED(PIPNET_EPI_BIAS)
-    PIPNET_RED(PIPNET_EPI_BIAS_GELU)
-    PIPNET_RED(PIPNET_EPI_RESID)
-    PIPNET_RED(PIPNET_EPI_MUL)
-    PIPNET_RED(PIPNET_EPI_BIAS_RELU)
-    PIPNET_RED(PIPNET_EPI_BIAS_RESID_RELU)
-    PIPNET_RED(PIPNET_EPI_GELU_BWD)
-    default: return PIPNET_ERR_ARG;
-  }
-#undef PIPNET_RED
-  PIPNET_CHECK_LAUNCH();
-  return PIPNET_OK;
 }
 
 extern "C" int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float* W, const float* bias,

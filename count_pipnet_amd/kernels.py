@@ -97,19 +97,6 @@ def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
     return max(1, min(-(-SPLITK_WG_PER_CU * cus // tiles), k // 256, 64))
 
 
-SKINNY = os.environ.get("PIPNET_SKINNY", "1") == "1"       # env: A/B runs (tools)
-
-
-def skinny_ok(m: int, n: int, k: int, a: Tensor, w: Tensor, r: Optional[Tensor], out: Tensor,
-              bias: Optional[Tensor] = None, scale: Optional[Tensor] = None) -> bool:
-    """M <= 64 products go to the register-streaming skinny GEMM (pipnet_linear_skinny_f32)."""
-    if not SKINNY or m == 0 or m > 64 or n % 64 or k % 32 or a.stride(0) % 4 or out.stride(0) % 4:
-        return False
-    al = lambda t: t is None or t.data_ptr() % 16 == 0      # noqa: E731
-    return (al(a) and al(w) and al(out) and al(bias) and al(scale)
-            and (r is None or (al(r) and r.stride(0) % 4 == 0)))
-
-
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
@@ -146,14 +133,6 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     if out is None:
         out = torch.empty((m, n), device=a.device, dtype=torch.float32)
     ldr = r.stride(0) if r is not None else 0
-    if skinny_ok(m, n, k, a, w, r, out, bias, scale):
-        sp = _lib.load().pipnet_skinny_splits(n, k)
-        ws = torch.empty((sp, m, n), device=a.device, dtype=torch.float32)
-        _launch(f"(anonymous namespace)::skinny_gemm_kernel<{2 if m > 32 else 1}>", 2.0 * m * n * k,
-                lambda: _lib.call("pipnet_linear_skinny_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias),
-                                  _ptr(scale), _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue,
-                                  ws.data_ptr(), _stream(a)))
-        return out
     splits = splitk_factor(m, n, k)
     if splits > 1:
         ws = torch.empty((splits, m, n), device=a.device, dtype=torch.float32)

@@ -88,17 +88,6 @@ int pipnet_linear_rowscale_f32(const float* A, int64_t lda, const float* W, cons
                                const float* R, int64_t ldr, float* C, int64_t ldc, int M, int N, int K,
                                const float* row_scale, int rows_per_scale, void* stream);
 
-/* Skinny-M products (M <= 64: the Bilinear intermediate at M = batch, count_pipnet_utils.py:
- * 342-385): each wave streams 64 columns of W and the A rows straight into registers (W is
- * read exactly once; no LDS staging), 4 waves per workgroup split the workgroup's K slab and
- * sum in wave order, the slabs land in `workspace` (pipnet_skinny_splits(N, K) * M * N floats)
- * and one reduction kernel sums them in slab order with the epilogue.  The slab split depends
- * on (N, K) only, so a row's result never depends on M.  N % 64 == 0, K % 32 == 0, M <= 64. */
-int pipnet_skinny_splits(int N, int K);
-int pipnet_linear_skinny_f32(const float* A, int64_t lda, const float* W, const float* bias,
-                             const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
-                             int M, int N, int K, int epilogue, float* workspace, void* stream);
-
 /* Split-K variant for short-M products (M <= a few hundred rows, long K: the Bilinear /
  * LinearFull intermediate GEMMs at M = batch, count_pipnet_utils.py:342-385): the K range
  * is cut into `splits` slabs computed by separate workgroups into `workspace`

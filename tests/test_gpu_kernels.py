@@ -410,32 +410,3 @@ def test_gemm_stream_bitwise(gpu, m, n, k, epi):
     elif epi == "bias":
         ref = ref + b.double()
     assert (outs[1][:m].double() - ref).abs().max().item() < 1e-3
-
-
-@pytest.mark.parametrize("m,n,k,epi", [
-    (64, 6144, 2048, "none"),     # C5 BilinearIntermediate embed at 64 images per GPU
-    (64, 6144, 6144, "mul"),      # C5 V(e) * W(e)
-    (33, 1024, 6144, "resid"),    # two row blocks, ragged
-    (32, 512, 256, "bias"),       # one row block, one K slab
-    (2, 6144, 6144, "none"),      # the golden's batch of 2
-    (1, 64, 96, "gelu"),          # K shorter than a workgroup slab
-])
-def test_linear_skinny(gpu, m, n, k, epi):
-    """Skinny-M GEMM (pipnet_linear_skinny_f32, M <= 64, register-streamed W): every epilogue
-    against fp64, and each row's result independent of M (bitwise: the slab split depends on
-    (N, K) only)."""
-    g = torch.Generator().manual_seed(m * 31 + n + k)
-    a, w = _rand(m, k, gen=g), _rand(n, k, gen=g, scale=0.05)
-    b, s, r = _rand(n, gen=g), _rand(n, gen=g), _rand(m, n, gen=g)
-    e = {"none": _lib.EPI_NONE, "mul": _lib.EPI_MUL, "resid": _lib.EPI_RESID, "bias": _lib.EPI_BIAS,
-         "gelu": _lib.EPI_BIAS_GELU}[epi]
-    acc = a @ w.t()
-    ref = {"none": acc, "mul": acc * r, "resid": r + s * (acc + b), "bias": acc + b, "gelu": F.gelu(acc + b)}[epi]
-    d = lambda t: t.float().to(gpu)  # noqa: E731
-    assert K.skinny_ok(m, n, k, d(a), d(w), d(r), torch.empty(m, n, device=gpu))
-    out = K.linear(d(a), d(w), d(b), e, scale=d(s), r=d(r)).double().cpu()
-    tol = 4e-6 * (1 + ref.abs()) + 4e-6 * ((a.abs() @ w.abs().t()) * (1 + s.abs() + r.abs()))
-    assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
-    if m > 1:
-        part = K.linear(d(a[1:2]), d(w), d(b), e, scale=d(s), r=d(r[1:2])).cpu()
-        assert torch.equal(part[0], out[1].float())
