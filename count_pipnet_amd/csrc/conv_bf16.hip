@@ -53,12 +53,18 @@ int conv_variant(int M, int N, bool pp_ok, bool s3 = false, int Kv = 0) {
     if (N == 384) return Kv >= 3 * 1024 ? 7 : m128;  // stage-3 Linear2: 192-wide; short K: 128x128
     return N >= 256 ? 5 : m128;
   }
-  if (N >= 256 && pp_ok) return 5;
+  const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
+  // K <= 64 (layer1 conv3: 64 -> 256 + identity): one K-tile pair per tile, all epilogue -- the
+  // 2-workgroup 128 x 128 tile overlaps one workgroup's epilogue with the other's MFMAs
+  // (41 vs 47 us per half batch, profiles/r03/conv_bf16_b64.log).  A per-layer rule (K, N).
+  if (N >= 256 && pp_ok && Kv > 64) return 5;
   if (N <= 64 && !s3) return 6;   // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
-  const int64_t tm = (int64_t)((M + 127) / 128) * ((N + 127) / 128);
-  if (N >= 256 && tl >= 256) return 3;
-  if (tm >= 512) return 4;
+  if (N >= 256 && tl >= 256 && Kv > 64) return 3;
+  // 128 x 128 once the grid covers each CU once (layer2 conv2 at 64 images: 392 tiles, 31-34 vs
+  // 42-44 us on 64 x 128); tiles 0 / 3 / 4 walk K identically, so this M-dependent choice keeps
+  // every pixel's result bitwise batch-invariant
+  if (tm >= 256) return 4;
   return 0;
 }
 
@@ -85,7 +91,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   // 1x1 convs with N % 256 == 0: the persistent ping-pong tile (9), same K order as tile 5
   const bool pk = ALOAD == ALOAD_DENSE && pp_ok && p.N % 256 == 0 && !is_s3_epi(epi);
   if (v < 0) {
-    v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv);
+    v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv > 0 ? p.Kv : p.K);
     if (hk) v = 8;
     else if (v == 5 && pk) v = 9;
   }

@@ -235,8 +235,9 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
     8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31, N >= 256),
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
-    6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 on 32x32x16
-    MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M."""
+    6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 / 8 / 9 on
+    32x32x16 MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M.
+    ``kv`` = KH*KW*Cin: layers with K <= 64 never take the single-workgroup ping-pong tiles."""
     if s3:
         m128 = 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
         if not pp_ok:
@@ -248,13 +249,14 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
         return 5 if n >= 256 else m128
     if halo_ok:
         return 8
-    if n >= 256 and pp_ok:
+    short_k = 0 < kv <= 64                  # layer1 conv3 / downsample (K = 64): 2-workgroup tiles
+    if n >= 256 and pp_ok and not short_k:
         return 9 if ppp_ok else 5
     if n <= 64 and not s3:
         return 6
-    if n >= 256 and -(-m // 256) * -(-n // 256) >= 256:
+    if n >= 256 and -(-m // 256) * -(-n // 256) >= 256 and not short_k:
         return 3
-    return 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
+    return 4 if -(-m // 128) * -(-n // 128) >= 256 else 0
 
 
 _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
@@ -317,7 +319,7 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
                and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     ppp_ok = (aload == 0 and pp_ok and cout % 256 == 0
               and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, halo_ok=halo_ok, ppp_ok=ppp_ok),
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok),
             2.0 * m * cout * k,
             lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
                               _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), tile,
