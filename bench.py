@@ -59,6 +59,9 @@ def parse_args(argv=None):
                     help="fp32: exact fp32 MFMA GEMMs; bf16x3: split-bf16 GEMMs (fp32 in/out, ~1e-5 per product)")
     ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
                     help="also time this precision on the same network (reported under alt_precision)")
+    ap.add_argument("--stream-split", type=int, default=None,
+                    help="override the model's default stream split for the throughput pass (profiling runs use 1 "
+                         "so every launch of a kernel is a full-batch launch, as in the roofline pass)")
     ap.add_argument("--dist-backend", default=None,
                     help="rehearsal only: torch.distributed backend (default nccl = RCCL on GPUs)")
     ap.add_argument("--device-index", type=int, default=None,
@@ -280,6 +283,9 @@ def main():
     # step ends with the RCCL all-gather of pooled + logits (DataParallel's gather)
     sharded = ShardedInference(net)
     xs = synth_images(a.batch, 224, seed=100 + rank).to(dev)
+    if a.stream_split is not None:
+        from count_pipnet_amd.pipnet import set_stream_split as _sss
+        _sss(net, a.stream_split)
 
     def barrier():
         if world > 1:
