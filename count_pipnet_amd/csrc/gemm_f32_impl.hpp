@@ -25,6 +25,8 @@
 // MFMA group of tile k.
 // General path (any K % 4): register staging with zero-fill of the K tail.
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 
 namespace pipnet_gemm {
@@ -212,6 +214,60 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, in
   }
 }
 
+// 16x16x4 accumulator set of a (32*TM)x64 wave tile: acc[ib][jb] is the 16x16 block at rows
+// ib*16.., columns jb*16..; register e of lane l holds row 4*(l>>4) + e, column l & 15.
+using Acc16 = f32x4[4][4];
+
+template <int EPI, int TM>
+PIPNET_DEV void epilogue(const GemmParams& p, const Acc16& acc, int m0, int n0, int wm, int wn, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    const int n = n0 + wn * 64 + jb * 16 + r16;
+    if (n >= p.N) continue;
+    float bn = 0.f, sn = 1.f;
+    if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && EPI != PIPNET_EPI_GELU_BWD) bn = p.bias ? p.bias[n] : 0.f;
+    if (EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) sn = p.scale ? p.scale[n] : 1.f;
+#pragma unroll
+    for (int ib = 0; ib < 2 * TM; ++ib) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * 32 * TM + ib * 16 + 4 * g + e;
+        if (m >= p.M) continue;
+        float x = acc[ib][jb][e];
+        if (EPI == PIPNET_EPI_BIAS) x = x + bn;
+        if (EPI == PIPNET_EPI_BIAS_GELU) x = gelu_fast(x + bn);
+        if (EPI == PIPNET_EPI_RESID) x = fmaf(sn, x + bn, p.R[(int64_t)m * p.ldr + n]);
+        if (EPI == PIPNET_EPI_RESID_ROWSCALE)
+          x = p.R[(int64_t)m * p.ldr + n] + p.row_scale[m / p.rows_per_scale] * (sn * (x + bn));
+        if (EPI == PIPNET_EPI_GELU_BWD) x = x * gelu_grad(p.R[(int64_t)m * p.ldr + n]);
+        if (EPI == PIPNET_EPI_MUL) x = x * p.R[(int64_t)m * p.ldr + n];
+        if (EPI == PIPNET_EPI_BIAS_RELU) x = fmaxf(x + bn, 0.f);
+        if (EPI == PIPNET_EPI_BIAS_RESID_RELU) x = fmaxf(x + bn + p.R[(int64_t)m * p.ldr + n], 0.f);
+        p.C[(int64_t)m * p.ldc + n] = x;
+      }
+    }
+  }
+}
+
+// 32-row slab i of a wave's accumulators -> its 32 x 64 LDS image (row-major), per MFMA layout
+PIPNET_DEV void slab_write(float* wt, const Acc& acc, int i, int lane) {
+  const int lr = lane & 31, lh = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * 64 + j * 32 + lr] = acc[i][j][v];
+}
+PIPNET_DEV void slab_write(float* wt, const Acc16& acc, int i, int lane) {
+  const int r16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wt[(h * 16 + 4 * g + e) * 64 + jb * 16 + r16] = acc[2 * i + h][jb][e];
+}
+
 template <int EPI>
 PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4& r, float rs = 1.f) {
   if (EPI == PIPNET_EPI_BIAS) x = x + bn;
@@ -260,13 +316,12 @@ PIPNET_DEV void st4_c(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinte
 // whole main loop on the K=96 GEMMs.  All residual float4 loads of a lane are issued
 // before the first store (one latency, not sixteen).  Needs N % 4 == 0, ldc / ldr % 4 ==
 // 0, 16-B aligned C / R, and 32 KiB of the kernel's LDS (free after the main loop).
-template <int EPI, int TM>
-PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, int m0, int n0, int wm, int wn,
+template <int EPI, int TM, class AccT>
+PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, int m0, int n0, int wm, int wn,
                              int lane, int wid) {
   constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU ||
                          EPI == PIPNET_EPI_RESID_ROWSCALE || EPI == PIPNET_EPI_GELU_BWD;
   float* wt = smem + wid * 32 * 64;
-  const int lr = lane & 31, lh = lane >> 5;
   const int c4 = lane & 15;
   const int n = n0 + wn * 64 + 4 * c4;
   const bool nok = n < p.N;
@@ -287,10 +342,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const Acc& acc, float* smem, i
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * 64 + j * 32 + lr] = acc[i][j][v];
+    slab_write(wt, acc, i, lane);
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
@@ -317,6 +369,13 @@ PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int in_group = tile - group * gm * p.nt;
   m0 = (first_m + in_group % gsz) * bm;
   n0 = (in_group / gsz) * BN;
+}
+
+PIPNET_DEV void zero_acc(Acc16& acc) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
 PIPNET_DEV void zero_acc(Acc& acc) {
@@ -379,6 +438,44 @@ PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
 }
 
+// v_mfma_f32_16x16x4_f32 operands (cdna_hip_programming.md section 3: lane l supplies
+// A[l & 15][k = l >> 4] and B[k = l >> 4][l & 15]).  Group q of a BK-deep LDS tile: lane group
+// g = l >> 4 reads logical chunk 4q + g (4 consecutive k) of row (l & 15) of every 16-row
+// block, so MFMA e of the group multiplies k = 4 (4q + g) + e in lane group g -- the same map
+// for both operands, so every k of the tile is summed once.  With the swz() XOR above every
+// ds_read_b128 lane group ({0-3,12-15,20-27}, ...) hits 16 distinct 16-B bank slots (BK 32).
+struct Frag16 {
+  f32x4 a[4], b[4];
+};
+
+template <int BK, int TM>
+PIPNET_DEV void read_frag16(Frag16& f, const float* buf, int wm, int wn, int lane, int q) {
+  using G = Geo<BK, TM>;
+  const int r16 = lane & 15, c = 4 * q + (lane >> 4);
+#pragma unroll
+  for (int ib = 0; ib < 2 * TM; ++ib) {
+    const int ra = wm * 32 * TM + ib * 16 + r16;
+    f.a[ib] = ld4(buf + ra * BK + 4 * G::swz(ra, c));
+  }
+#pragma unroll
+  for (int jb = 0; jb < 4; ++jb) {
+    const int rb = wn * 64 + jb * 16 + r16;
+    f.b[jb] = ld4(buf + G::BMT * BK + rb * BK + 4 * G::swz(rb, c));
+  }
+}
+
+// JL = active 32-column blocks of the wave (NPAD), i.e. 2 * JL 16-column blocks
+template <int TM, int JL = 2>
+PIPNET_DEV void mfma_frag16(Acc16& acc, const Frag16& f) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int ib = 0; ib < 2 * TM; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 2 * JL; ++jb)
+        acc[ib][jb] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[ib][e], f.b[jb][e], acc[ib][jb], 0, 0, 0);
+}
+
 template <int V>
 struct IntC {
   static constexpr int value = V;
@@ -403,16 +500,18 @@ PIPNET_DEV void wait_dma_barrier() {
 // NPAD (grids whose N % 128 != 0): MFMA blocks of columns >= N are skipped, and the wave ->
 // column-half map flips with the workgroup parity, so the lighter waves of co-resident
 // workgroups land on different SIMDs (a relabelling: every output is computed identically).
-template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false>
-__global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
+// SH = MFMA shape: 0 = v_mfma_f32_32x32x2_f32, 1 = v_mfma_f32_16x16x4_f32 (same tile, LDS image,
+// DMA and fragment bytes; a different k order inside each K-tile, so a different rounding).
+template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD>
+PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
   using G = Geo<BK, TM>;
+  static_assert(SH == 0 || BK == 32, "16x16x4 fragments: BK 32 (the swizzle is conflict-free there)");
   // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
   const int nk_all = p.K / BK;
   const int kt_begin = (int)((int64_t)nk_all * blockIdx.y / gridDim.y);
   const int nk = (int)((int64_t)nk_all * (blockIdx.y + 1) / gridDim.y) - kt_begin;
   p.C += (int64_t)blockIdx.y * p.split_stride;
   constexpr int DMA_PER_TILE = G::A_DMA + G::B_DMA;     // per wave
-  __shared__ __attribute__((aligned(16))) float smem[NS * G::TILE_FLOATS];
   static_assert(NS * G::TILE_FLOATS >= 4 * 32 * 64, "vector epilogue needs 32 KiB of LDS");
 
   const int tid = threadIdx.x;
@@ -493,7 +592,8 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
     }
   };
 
-  Acc acc;
+  using AccT = typename std::conditional<SH == 0, Acc, Acc16>::type;
+  AccT acc;
   zero_acc(acc);
   lab_stamp<ABL>(p, 0);
 
@@ -505,6 +605,29 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   // branch here instead of one per MFMA group
   auto main_loop = [&](auto jlc) {
     constexpr int JL = decltype(jlc)::value;
+    if constexpr (SH == 1) {
+      // 2 fragment groups of 64 MFMAs (2048 cycles per wave) per 32-deep K-tile
+      Frag16 fa, fb;
+      read_frag16<BK, TM>(fa, smem, wm, wn, lane, 0);
+      int cur = 0;
+      for (int kt = 0; kt < nk; ++kt) {
+        const float* buf = smem + cur * G::TILE_FLOATS;
+        if (kt + NS - 1 < nk) {
+          int nb = cur + NS - 1;
+          if (nb >= NS) nb -= NS;
+          stage(kt + NS - 1, nb);
+          issued = kt + NS - 1;
+        }
+        read_frag16<BK, TM>(fb, buf, wm, wn, lane, 1);
+        mfma_frag16<TM, JL>(acc, fa);
+        const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
+        if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);
+        if (kt + 1 < nk) read_frag16<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lane, 0);
+        mfma_frag16<TM, JL>(acc, fb);
+        cur = nxt;
+      }
+      return;
+    } else {
     Frag fa, fb;
     read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
     int cur = 0;
@@ -533,6 +656,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
       mfma_frag<TM, JL>(acc, fb);
       cur = nxt;
     }
+    }
   };
   if constexpr (NPAD) {
     if (jl >= 2) main_loop(IntC<2>{});
@@ -543,24 +667,36 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
   }
   lab_stamp<ABL>(p, 2);
   if (ABL & 2) {
+    const float* av = reinterpret_cast<const float*>(&acc);
     float t = 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int v = 0; v < 16; ++v) t += acc[i][j][v];
+    for (int v = 0; v < 64; ++v) t += av[v];
     p.C[(int64_t)blockIdx.x * NTHREADS + tid] = t;
     return;
   }
   if (p.vec_epi)
     epilogue_vec<EPI, TM>(p, acc, smem, m0, n0, wm, wn, lane, wid);
-  else
+  else if constexpr (SH == 0)
     epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lr, lh);
+  else
+    epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lane);
   if constexpr ((ABL & 8) != 0) {
     __syncthreads();
     lab_stamp<ABL>(p, 3);
   }
+}
+
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false>
+__global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM>::TILE_FLOATS];
+  gemm_tn_body<0, BK, TM, EPI, ALOAD, NS, ABL, NPAD>(p, smem);
+}
+
+// the same tile on v_mfma_f32_16x16x4_f32
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false>
+__global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn16_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM>::TILE_FLOATS];
+  gemm_tn_body<1, BK, TM, EPI, ALOAD, NS, ABL, NPAD>(p, smem);
 }
 
 // ======================================================================================

@@ -4,8 +4,21 @@
 
 using namespace pipnet_gemm;
 
-template <int BK, int TM, int MINB, int NS, int ABL = 0>
+template <int BK, int TM, int MINB, int NS, int ABL = 0, int SH = 0>
 static void launch(GemmParams& p, int epi, hipStream_t s) {
+  if constexpr (SH == 1) {
+    p.mt = (p.M + 64 * TM - 1) / (64 * TM);
+    const dim3 grid(p.mt * p.nt), block(NTHREADS);
+    if (epi == PIPNET_EPI_BIAS_GELU)
+      hipLaunchKernelGGL((gemm_f32_tn16_kernel<BK, TM, PIPNET_EPI_BIAS_GELU, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+    else if (epi == PIPNET_EPI_BIAS)
+      hipLaunchKernelGGL((gemm_f32_tn16_kernel<BK, TM, PIPNET_EPI_BIAS, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+    else if (epi == PIPNET_EPI_RESID)
+      hipLaunchKernelGGL((gemm_f32_tn16_kernel<BK, TM, PIPNET_EPI_RESID, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+    else
+      hipLaunchKernelGGL((gemm_f32_tn16_kernel<BK, TM, PIPNET_EPI_NONE, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+    return;
+  }
   p.mt = (p.M + 64 * TM - 1) / (64 * TM);
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
   if (epi == PIPNET_EPI_BIAS_GELU)
@@ -61,6 +74,11 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 30: launch<32, 2, 2, 2, 8>(p, epi, s); break;
     case 32: launch<32, 1, 3, 2, 8>(p, epi, s); break;
     case 33: launch<16, 2, 2, 3, 8>(p, epi, s); break;
+    // v_mfma_f32_16x16x4_f32 forms of variants 0 / 2 / 1, and a stamped copy of 40
+    case 40: launch<32, 2, 2, 2, 0, 1>(p, epi, s); break;
+    case 42: launch<32, 1, 3, 2, 0, 1>(p, epi, s); break;
+    case 41: launch<32, 1, 2, 2, 0, 1>(p, epi, s); break;
+    case 70: launch<32, 2, 2, 2, 8, 1>(p, epi, s); break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
