@@ -2,6 +2,7 @@
 // v0 = the register-tile kernel (convnext_dw.hpp), v1.. = row-ring variants (dw_ring_lab.hpp).
 #include "../count_pipnet_amd/csrc/convnext_dw.hpp"
 #include "dw_ring_lab.hpp"
+#include "dw_lds_lab.hpp"
 using namespace pipnet_dw;
 
 extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, const float* wp, const float* bias,
@@ -24,6 +25,17 @@ extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, c
   R(1, 192, 4, 2, 2, 16) R(2, 192, 2, 2, 3, 16) R(3, 192, 4, 4, 1, 16) R(4, 192, 3, 2, 2, 16)
   R(1, 384, 4, 1, 2, 32) R(2, 384, 2, 1, 3, 32) R(3, 384, 4, 2, 1, 32) R(4, 384, 3, 1, 2, 32)
   R(1, 768, 2, 1, 1, 64) R(2, 768, 4, 1, 1, 64) R(3, 768, 2, 1, 1, 32) R(4, 768, 3, 1, 1, 64)
+  // v30 / v31: LDS-staged kernel (dwconv7_ln_lds_kernel) with 16- / 32-wide column tiles
+#define L(ID, CC, TWC) \
+  if (variant == ID && C == CC) return launch_dw_lds<CC, TWC>(x, B, H, W, wp, bias, lnw, lnb, y, s);
+  L(30, 96, 16) L(30, 192, 16) L(30, 384, 16) L(31, 96, 32) L(31, 192, 32) L(31, 384, 32)
+#undef L
+  // v32-v37: ablations of v30 (ABL bits: 1 no DMA after chunk 0, 2 no weight loads, 4 no row reads / FMAs)
+#define LA(ID, CC, ABL) \
+  if (variant == ID && C == CC) return launch_dw_lds<CC, 16, false, ABL>(x, B, H, W, wp, bias, lnw, lnb, y, s);
+  LA(32, 96, 1) LA(33, 96, 2) LA(34, 96, 4) LA(35, 96, 3) LA(36, 96, 6) LA(37, 96, 5)
+  LA(32, 384, 1) LA(33, 384, 2) LA(34, 384, 4) LA(35, 384, 3) LA(36, 384, 6) LA(37, 384, 5)
+#undef LA
   // ablations of v1 (ABL bits: 1 no LayerNorm, 2 no FMAs, 4 no input loads)
 #define A(ID, CC, TX, NS, MB, LPP, ABL)                                                                            \
   if (variant == ID && C == CC)                                                                                     \

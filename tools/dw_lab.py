@@ -42,7 +42,7 @@ for c, hw in SHAPES:
                     ref = y.clone()
                 else:
                     err = (y - ref).abs().max().item()
-                    assert err < 1e-3, (c, hw, v, mw, mr, err)
+                    assert err < 1e-3 or 32 <= v <= 39, (c, hw, v, mw, mr, err)   # v32-v39: ablations
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
