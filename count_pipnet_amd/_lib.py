@@ -84,6 +84,7 @@ SIGNATURES = {
     "pipnet_dwconv7_wgrad_f32": [P, P, I32, I32, I32, I32, P, P, I32, P, P],
     "pipnet_head_bwd_f32": [P, P, I32, I32, I32, P, P, I32, F32, F32, F32, P, P, P, P],
     "pipnet_cnblock_mlp_f32": [P, P, P, P, P, P, P, I64, I32, P],
+    "pipnet_cnblock_mlp_hw_f32": [P, P, P, P, P, P, P, I64, I32, I32, P],
     "pipnet_bn_workspace_floats": [I32],
     "pipnet_bn_stats_f32": [P, I64, I32, F32, F32, P, P, P, P, P, P],
     "pipnet_bn_apply_f32": [P, I64, I32, P, P, P, P, P, I32, P, P],

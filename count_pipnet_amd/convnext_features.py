@@ -259,7 +259,7 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
     if row_scale is None and c in K.MLP_FUSED_CHANNELS and FUSED_MLP \
             and hh * ww >= MLP_FUSED_MIN_PIXELS[c]:
         # narrow stages: Linear1 + GELU + Linear2 + layer_scale + residual in one kernel
-        K.cnblock_mlp(t.view(-1, c), l1.weight, l1.bias, l2.weight, l2.bias, blk.layer_scale.view(-1), hv)
+        K.cnblock_mlp(t.view(-1, c), l1.weight, l1.bias, l2.weight, l2.bias, blk.layer_scale.view(-1), hv, hw=hh * ww)
         return h
     u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS_GELU)
     if row_scale is None:

@@ -246,10 +246,17 @@ bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float*
                             const float* gamma, float* x, int M, hipStream_t s);
 #endif
 
-extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2,
-                                      const float* b2, const float* gamma, float* x, int64_t M, int C,
-                                      void* stream) {
-  if (M < 0 || M >= ((int64_t)1 << 31) || (C != 96 && C != 192)) return PIPNET_ERR_ARG;
+// Small maps (C = 192, <= 16 x 16 pixels per image: C5's stage 2) split the hidden dimension
+// over two waves per 16-pixel group (HS = 2): 16384 pixels give 1024 pixel groups, one wave per
+// SIMD at HS = 1 (tools/mlp_lab.py, profiles/r02/mlp_lab.txt: 103 -> 93 us).  HS changes the
+// hidden summation order, so it is chosen from the layer's map size only -- never from M -- and
+// a pixel's result stays independent of the batch it runs in.
+constexpr int MLP_HS2_MAX_HW = 256;
+
+extern "C" int pipnet_cnblock_mlp_hw_f32(const float* t, const float* W1, const float* b1, const float* W2,
+                                         const float* b2, const float* gamma, float* x, int64_t M, int C, int hw,
+                                         void* stream) {
+  if (M < 0 || M >= ((int64_t)1 << 31) || (C != 96 && C != 192) || hw < 0) return PIPNET_ERR_ARG;
   if (!t || !W1 || !b1 || !W2 || !b2 || !gamma || !x) return PIPNET_ERR_ARG;
   if (!aligned16(t) || !aligned16(W1) || !aligned16(b1) || !aligned16(W2) || !aligned16(b2) || !aligned16(gamma) ||
       !aligned16(x))
@@ -267,8 +274,16 @@ extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const flo
     if (m >= 8192) return launch_mlp<96, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
     return launch_mlp<96, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   }
+  if (hw > 0 && hw <= MLP_HS2_MAX_HW) return launch_mlp<192, 16, 8, 1, 2>(t, W1, b1, W2, b2, gamma, x, m, s);  // C5 stage 2
   if (m >= 32768) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);      // C2 stage 2
-  if (m >= 8192) return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);       // C5 stage 2
+  if (m >= 8192) return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   if (m >= 4096) return launch_mlp<192, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   return launch_mlp<192, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+}
+
+// map size unknown: the HS = 1 instantiations only
+extern "C" int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2,
+                                      const float* b2, const float* gamma, float* x, int64_t M, int C,
+                                      void* stream) {
+  return pipnet_cnblock_mlp_hw_f32(t, W1, b1, W2, b2, gamma, x, M, C, 0, stream);
 }

@@ -382,8 +382,13 @@ def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tens
 MLP_FUSED_CHANNELS = (96, 192)
 
 
-def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20) -> str:
-    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_f32)."""
+MLP_HS2_MAX_HW = 256    # C = 192 on maps of <= 16 x 16: hidden split over two waves (csrc/mlp_f32.hip)
+
+
+def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20, hw: int = 0) -> str:
+    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32)."""
+    if c == 192 and 0 < hw <= MLP_HS2_MAX_HW:
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
     if c == 96:
         nw = 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
         return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
@@ -393,10 +398,12 @@ def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20) -> str:
     return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
 
 
-def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor) -> Tensor:
+def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor,
+                hw: int = 0) -> Tensor:
     """In place on ``x`` [M, C]: x += gamma * (W2 gelu(W1 t + b1) + b2) -- the whole CNBlock MLP
     of a narrow stage (C = 96 / 192) in one kernel, the hidden activation kept in registers
-    (csrc/mlp_f32.hip)."""
+    (csrc/mlp_f32.hip).  ``hw`` = the layer's pixels per image (0 = unknown): picks the
+    instantiation by map size, never by M."""
     for v, what in ((t, "mlp input"), (w1, "fc1 weight"), (b1, "fc1 bias"), (w2, "fc2 weight"), (b2, "fc2 bias"),
                     (gamma, "layer scale"), (x, "residual")):
         _chk(v, what)
@@ -404,9 +411,9 @@ def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma
     if c not in MLP_FUSED_CHANNELS or tuple(x.shape) != (m, c) or tuple(w1.shape) != (4 * c, c) \
             or tuple(w2.shape) != (c, 4 * c) or b1.numel() != 4 * c or b2.numel() != c or gamma.numel() != c:
         raise RuntimeError(f"cnblock_mlp: shapes t {tuple(t.shape)} w1 {tuple(w1.shape)} w2 {tuple(w2.shape)}")
-    _launch(cnblock_mlp_kernel_name(c, m), 2.0 * 2 * m * 4 * c * c,
-            lambda: _lib.call("pipnet_cnblock_mlp_f32", t.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
-                              b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), m, c, _stream(t)))
+    _launch(cnblock_mlp_kernel_name(c, m, hw), 2.0 * 2 * m * 4 * c * c,
+            lambda: _lib.call("pipnet_cnblock_mlp_hw_f32", t.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(),
+                              b2.data_ptr(), gamma.data_ptr(), x.data_ptr(), m, c, hw, _stream(t)))
     return x
 
 

@@ -259,6 +259,11 @@ int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mo
  * leaves the registers.  All pointers 16-B aligned. */
 int pipnet_cnblock_mlp_f32(const float* t, const float* W1, const float* b1, const float* W2, const float* b2,
                            const float* gamma, float* x, int64_t M, int C, void* stream);
+/* Same, told the layer's feature-map size hw = H*W per image (0 = unknown, as above): C = 192 on
+ * maps of <= 256 pixels splits the hidden dimension over two waves per 16-pixel group (another
+ * fixed summation order, chosen by hw only, so a pixel's result never depends on M). */
+int pipnet_cnblock_mlp_hw_f32(const float* t, const float* W1, const float* b1, const float* W2, const float* b2,
+                              const float* gamma, float* x, int64_t M, int C, int hw, void* stream);
 
 /* NonNegLinear (pipnet.py:54-71, count_pipnet.py:176-224): out = x' relu(W)^T + b with
  * x' = where(x < thresh, 0, x) when apply_thresh (pipnet.py:36, inference) else x.

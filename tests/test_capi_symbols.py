@@ -101,6 +101,7 @@ def test_roofline_kernel_names_exist_in_library():
     for c, m in [(96, 200704), (96, 20000), (96, 9000), (96, 4096), (192, 50176), (192, 16384), (192, 5000),
                  (192, 1024)]:                                 # fused narrow-stage MLP (csrc/mlp_f32.hip)
         assert K.cnblock_mlp_kernel_name(c, m) in out, (c, m)
+    assert K.cnblock_mlp_kernel_name(192, 16384, hw=256) in out          # hidden split (C5 stage 2)
     for m, n, epi, s3 in [(200704, 96, _lib.EPI_F32_RESID, True), (200704, 384, _lib.EPI_S3_GELU, True),
                           (50176, 192, _lib.EPI_F32_RESID, True), (401408, 64, _lib.EPI_BIAS_RELU, False),
                           (100352, 128, _lib.EPI_BIAS_RELU, False)]:

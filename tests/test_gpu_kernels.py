@@ -297,6 +297,31 @@ def test_cnblock_mlp_fused(gpu, c, m):
     assert torch.allclose(xo, xu, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("m", [16384, 777, 3])
+def test_cnblock_mlp_fused_hidden_split(gpu, m):
+    """C = 192 on a <= 16 x 16 map (C5's stage 2): the hidden dimension split over two waves
+    per pixel group (HS = 2, chosen by the map size) against fp64 torch, ragged M; and it does
+    not depend on M (bitwise, prefixes of the batch)."""
+    c, hw = 192, 256
+    g = torch.Generator().manual_seed(c + m + hw)
+    t, x = _rand(m, c, gen=g), _rand(m, c, gen=g)
+    w1, b1 = _rand(4 * c, c, gen=g, scale=0.1), _rand(4 * c, gen=g, scale=0.5)
+    w2, b2 = _rand(c, 4 * c, gen=g, scale=0.05), _rand(c, gen=g)
+    gm = _rand(c, gen=g)
+    hid = F.gelu(t @ w1.t() + b1)
+    ref = x + gm * (hid @ w2.t() + b2)
+    d = lambda v: v.float().to(gpu).contiguous()  # noqa: E731
+    xo = d(x)
+    K.cnblock_mlp(d(t), d(w1), d(b1), d(w2), d(b2), d(gm), xo, hw=hw)
+    out = xo.double().cpu()
+    tol = 4e-6 * (gm.abs() * ((hid.abs() @ w2.abs().t()) + (t.abs() @ w1.abs().t()).mean())) + 1e-5
+    assert torch.all((out - ref).abs() <= tol), (out - ref).abs().max()
+    for rows in {m // 2 + 1, 1}:
+        part = d(x[:rows])
+        K.cnblock_mlp(d(t[:rows]), d(w1), d(b1), d(w2), d(b2), d(gm), part, hw=hw)
+        assert torch.equal(part, xo[:rows]), rows
+
+
 def test_cnblock_mlp_rejects_unsupported(gpu):
     z = torch.zeros(4, 384, device=gpu)
     with pytest.raises(RuntimeError):
