@@ -50,6 +50,7 @@ SIGNATURES = {
     "pipnet_layernorm_s3": [P, I64, I32, P, P, P, P],
     "pipnet_maxpool2d_nhwc_bf16": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_bf16": [P, I32, I32, I32, I32, I32, P, P],
+    "pipnet_nchw_to_s2d_bf16": [P, I32, I32, I32, P, P],
     "pipnet_softmax_pool_bf16": [P, I32, I32, I32, I32, P, P, P],
     "pipnet_eval_batch_f32": [P, P, P, I32, I32, I32, P, P, F32, P, P, P, P, P, P, P],
     "pipnet_weight_sparsify_f32": [P, I64, F32, P],

@@ -243,6 +243,34 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_bf16_kernel(const float* __r
   }
 }
 
+// The ResNet stem (Conv2d 3 -> 64, k7 s2 p3) as a 4x4 / stride-1 / pad-0 conv over a 2x2
+// space-to-depth image: S[b][i][j][q], q = (2 bi + bj) * 4 + c, holds x[b][c][2(i-2)+bi][2(j-2)+bj]
+// (zero outside the image and in the c = 3 slots), SH = OH + 3, SW = OW + 3.  With the weights
+// re-laid as W'[o][a][a'][q] = w[o][c][2a+bi-1][2a'+bj-1] (zero where the tap index is -1) the
+// conv has K = 4*4*16 = 256 instead of 7*7*8 = 392 -> 448 padded: 1.75x fewer MFMAs and A-operand
+// bytes for the same outputs (every product of the 7x7 conv appears once; the extra ones are
+// exact zeros).  One thread per S pixel: 12 reads, two 16-B stores.
+__global__ __launch_bounds__(256) void nchw_to_s2d_bf16_kernel(const float* __restrict__ x, int B, int H, int W,
+                                                               int SH, int SW, bf16* __restrict__ y) {
+  const int64_t n = (int64_t)B * SH * SW;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / ((int64_t)SH * SW);
+    const int rem = (int)(i - b * SH * SW);
+    const int si = rem / SW, sj = rem - (rem / SW) * SW;
+    bf16x8 o[2];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int bi = q >> 3, bj = (q >> 2) & 1, c = q & 3;
+      const int r = 2 * (si - 2) + bi, cc = 2 * (sj - 2) + bj;
+      float v = 0.f;
+      if (c < 3 && (unsigned)r < (unsigned)H && (unsigned)cc < (unsigned)W) v = x[((b * 3 + c) * H + r) * W + cc];
+      o[q >> 3][q & 7] = (bf16)v;
+    }
+    *reinterpret_cast<bf16x8*>(y + i * 16) = o[0];
+    *reinterpret_cast<bf16x8*>(y + i * 16 + 8) = o[1];
+  }
+}
+
 // MaxPool2d on NHWC bf16, 8 channels (16 B) per thread; max is exact in bf16 and padding
 // never wins (torch pads max-pool with -inf).
 __global__ __launch_bounds__(256) void maxpool_nhwc_bf16_kernel(const bf16* __restrict__ x, int B, int H, int W,
@@ -331,6 +359,17 @@ extern "C" int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int
   if (B == 0) return PIPNET_OK;
   hipLaunchKernelGGL(nchw_to_nhwc_bf16_kernel, dim3(grid_for((int64_t)B * H * W)), dim3(256), 0,
                      (hipStream_t)stream, x, B, C, H, W, Cpad, reinterpret_cast<bf16*>(y));
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
+extern "C" int pipnet_nchw_to_s2d_bf16(const float* x, int B, int H, int W, void* y, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || !x || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(y)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  const int SH = (H - 1) / 2 + 4, SW = (W - 1) / 2 + 4;
+  hipLaunchKernelGGL(nchw_to_s2d_bf16_kernel, dim3(grid_for((int64_t)B * SH * SW)), dim3(256), 0, (hipStream_t)stream,
+                     x, B, H, W, SH, SW, reinterpret_cast<bf16*>(y));
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }

@@ -344,6 +344,27 @@ def nchw_to_nhwc_bf16(x: Tensor, cpad: int) -> Tensor:
     return y
 
 
+def nchw_to_s2d_bf16(x: Tensor) -> Tensor:
+    """[B,3,H,W] fp32 -> [B, (H-1)//2 + 4, (W-1)//2 + 4, 16] bf16 space-to-depth stem input
+    (pipnet_nchw_to_s2d_bf16): the k7 s2 p3 ResNet stem becomes a 4x4 stride-1 conv over it."""
+    _chk(x, "network input (NCHW)")
+    b, c, h, w = x.shape
+    if c != 3:
+        raise RuntimeError(f"nchw_to_s2d_bf16: expects 3 channels, got {c}")
+    y = torch.empty((b, (h - 1) // 2 + 4, (w - 1) // 2 + 4, 16), device=x.device, dtype=torch.bfloat16)
+    _lib.call("pipnet_nchw_to_s2d_bf16", x.data_ptr(), b, h, w, y.data_ptr(), _stream(x))
+    return y
+
+
+def stem_weight_s2d(w_ohwi: Tensor) -> Tensor:
+    """[Cout, 7, 7, 3] (fp32, BatchNorm folded) -> [Cout, 4, 4, 16]: the taps of the k7 s2 conv
+    regrouped for the 4x4 conv over the space-to-depth image, W'[o][a][a'][(2 bi + bj) * 4 + c] =
+    w[o][2a+bi-1][2a'+bj-1][c], zero for the tap index -1 and the c = 3 slot."""
+    co = w_ohwi.shape[0]
+    w8 = torch.nn.functional.pad(w_ohwi, (0, 1, 1, 0, 1, 0))            # [Cout, 8 (ky+1), 8 (kx+1), 4]
+    return w8.view(co, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(co, 4, 4, 16).contiguous()
+
+
 def _head_out(out, b, h, w, p, dev):
     """Caller-provided (proto [B,h,w,P], pooled [B,P]) fp32 contiguous outputs, or new ones."""
     if out is None:

@@ -56,6 +56,19 @@ def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Opti
     return ent[1]
 
 
+def _stem_s2d(cache: Dict, conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    """Folded stem weights re-laid for the space-to-depth 4x4 conv (kernels.stem_weight_s2d),
+    bf16-packed; rebuilt whenever the BatchNorm fold is."""
+    w, b = _fold(cache, "stem.f32", conv, bn)                   # [64, 7, 7, 3] fp32
+    ck = ("stem.s2d", str(w.device))
+    ent = cache.get(ck)
+    if ent is None or ent[0] is not w:
+        with torch.no_grad():
+            ent = (w, K.pack_conv_weight_bf16(K.stem_weight_s2d(w)))
+        cache[ck] = ent
+    return ent[1], b
+
+
 def _conv_bn(cache, key, conv, bn, x, epilogue, r=None, cpad=None):
     if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
         raise RuntimeError(f"ResNet HIP path: unsupported conv {conv}")
@@ -95,8 +108,15 @@ def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
     if not (mp.kernel_size == 3 and mp.stride == 2 and mp.padding == 1):
         raise RuntimeError(f"ResNet HIP path: unsupported stem pool {mp}")
     if getattr(model, "hip_dtype", torch.float32) == torch.bfloat16:
-        h = K.nchw_to_nhwc_bf16(x, 8)
-        h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=8)
+        c1 = model.conv1
+        if c1.kernel_size == (7, 7) and c1.stride == (2, 2) and c1.padding == (3, 3) and c1.groups == 1 \
+                and c1.dilation == (1, 1):
+            # space-to-depth stem: a 4x4 stride-1 conv with K = 256 instead of 7x7x8 -> 448
+            w, b = _stem_s2d(cache, c1, model.bn1)
+            h = K.conv2d_nhwc_bf16(K.nchw_to_s2d_bf16(x), w, 4, 4, b, 1, 0, _lib.EPI_BIAS_RELU)
+        else:
+            h = K.nchw_to_nhwc_bf16(x, 8)
+            h = _conv_bn(cache, "stem", c1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=8)
         h = K.maxpool2d_nhwc_bf16(h, 3, 2, 1)
     else:
         h = K.nchw_to_nhwc(x, 4)

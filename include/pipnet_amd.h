@@ -204,6 +204,12 @@ int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k,
 /* fp32 NCHW -> bf16 NHWC (round to nearest even), channels zero-padded to Cpad (% 8 == 0). */
 int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y, void* stream);
 
+/* ResNet stem input for a 3-channel k7 s2 p3 conv run as a 4x4 stride-1 conv: fp32 NCHW [B,3,H,W]
+ * -> bf16 2x2 space-to-depth image [B, SH, SW, 16], SH = (H-1)/2 + 4, SW = (W-1)/2 + 4,
+ * y[b][i][j][(2 bi + bj) * 4 + c] = x[b][c][2(i-2)+bi][2(j-2)+bj] (zero outside the image and for
+ * c = 3).  The matching weights are W'[o][a][a'][(2 bi + bj) * 4 + c] = w[o][c][2a+bi-1][2a'+bj-1]. */
+int pipnet_nchw_to_s2d_bf16(const float* x, int B, int H, int W, void* y, void* stream);
+
 /* pipnet_softmax_pool_f32 reading bf16 logits (fp32 softmax, fp32 proto / pooled out). */
 int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
                              float* pooled, void* stream);

@@ -220,6 +220,27 @@ def test_maxpool_relayout_softmax_bf16(gpu):
             assert torch.allclose(pooled.double().cpu(), rp, atol=1e-6, rtol=1e-5)
 
 
+@pytest.mark.parametrize("h,w", [(224, 224), (37, 30), (17, 19)])
+def test_stem_s2d_bf16(gpu, h, w):
+    """The space-to-depth stem of the bf16 ResNet path: the relayout kernel bit-exact against
+    its CPU restatement (tests/test_stem_s2d.py), and relayout + regrouped weights + the 4x4
+    bf16 conv (+ bias + ReLU) against the fp64 7x7 stride-2 conv of the same bf16 values."""
+    from test_stem_s2d import s2d_reference
+    g = torch.Generator().manual_seed(h + 7 * w)
+    x = torch.randn(2, 3, h, w, generator=g)
+    s = K.nchw_to_s2d_bf16(x.to(gpu)).cpu()
+    assert torch.equal(s, s2d_reference(x).to(torch.bfloat16))
+    wt = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    b = torch.randn(64, generator=g)
+    wp = K.pack_conv_weight_bf16(K.stem_weight_s2d(wt.permute(0, 2, 3, 1).contiguous()).to(gpu))
+    out = K.conv2d_nhwc_bf16(K.nchw_to_s2d_bf16(x.to(gpu)), wp, 4, 4, b.to(gpu), 1, 0, _lib.EPI_BIAS_RELU)
+    xb, wb = x.to(torch.bfloat16).double(), wt.to(torch.bfloat16).double()
+    ref = torch.relu(F.conv2d(xb, wb, b.double(), stride=2, padding=3)).permute(0, 2, 3, 1)
+    assert out.shape == ref.shape
+    err = (out.double().cpu() - ref).abs()
+    assert torch.all(err <= 1e-2 * (1 + ref.abs())), err.max()      # bf16 output rounding (2^-8)
+
+
 def _c3_bf16(gpu, num_features=0):
     from golden_util import golden_args, golden_inputs, golden_state_dict, load_golden
     from model_util import build_model
