@@ -51,6 +51,7 @@ SIGNATURES = {
     "pipnet_maxpool2d_nhwc_bf16": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_bf16": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_s2d_bf16": [P, I32, I32, I32, P, P],
+    "pipnet_conv1x1_bf16_dual": [P, I64, I32, P, P, I32, P, I32, P, P],
     "pipnet_softmax_pool_bf16": [P, I32, I32, I32, I32, P, P, P],
     "pipnet_eval_batch_f32": [P, P, P, I32, I32, I32, P, P, F32, P, P, P, P, P, P, P],
     "pipnet_weight_sparsify_f32": [P, I64, F32, P],
@@ -101,6 +102,7 @@ EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_RESID, EPI_MUL, EPI_BIAS_RELU, EPI_BIAS_R
 EPI_RESID_ROWSCALE = 7
 EPI_GELU_BWD = 8
 EPI_S3_GELU, EPI_F32_BIAS, EPI_F32_RESID = 9, 10, 11      # split-bf16 ("bf16x3") ConvNeXt path
+EPI_DUAL_BIAS_RELU = 12        # pipnet_conv1x1_bf16_dual: downsample + conv1 of a first Bottleneck
 
 ABI_VERSION = 2          # include/pipnet_amd.h PIPNET_AMD_ABI_VERSION
 

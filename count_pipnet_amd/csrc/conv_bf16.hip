@@ -111,11 +111,15 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
       case PIPNET_EPI_BIAS_RESID_RELU:
         hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(512), 0, s, p);
         break;
+      case PIPNET_EPI_DUAL_BIAS_RELU:
+        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_DUAL_BIAS_RELU>), grid, dim3(512), 0, s, p);
+        break;
       default: return PIPNET_ERR_ARG;
     }
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }
+  if (epi == PIPNET_EPI_DUAL_BIAS_RELU) return PIPNET_ERR_ARG;   // persistent 1x1 tile only
   if (v == 8) {                                  // ping-pong with the LDS input halo, 256 x 64 NB
     const int nb = halo_nb(p.N);
     p.nt = (p.N + 64 * nb - 1) / (64 * nb);
@@ -350,6 +354,32 @@ extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int C
                                        const void* R, int epilogue, void* y, void* stream) {
   return pipnet_conv2d_nhwc_bf16_tile(x, B, H, W, Cin, w_packed, bias, Cout, KH, KW, stride, pad, R, epilogue, y, -1,
                                       stream);
+}
+
+extern "C" int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias,
+                                        int N1, void* y1, int N2, void* y2, void* stream) {
+  if (M < 0 || M >= ((int64_t)1 << 31) || Cin <= 0 || (Cin & 7) || N1 <= 0 || N2 <= 0 || (N1 % 256) || (N2 % 256) ||
+      !x || !w_packed || !y1 || !y2)
+    return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y1) || !aligned16(y2) || (bias && !aligned16(bias)))
+    return PIPNET_ERR_ALIGN;
+  if (M == 0) return PIPNET_OK;
+  ConvParams p{};
+  p.A = reinterpret_cast<const bf16*>(x);
+  p.lda = Cin;
+  p.W = reinterpret_cast<const bf16*>(w_packed);
+  p.bias = bias;
+  p.C = reinterpret_cast<bf16*>(y1);
+  p.ldc = N1;
+  p.C2 = reinterpret_cast<bf16*>(y2);
+  p.ldc2 = N2;
+  p.nsplit = N1;
+  p.M = (int)M; p.N = N1 + N2;
+  p.Kv = Cin;
+  p.K = (Cin + KPAD - 1) / KPAD * KPAD;
+  p.H = (int)M; p.Wd = 1; p.Cin = Cin; p.OH = (int)M; p.OW = 1; p.stride = 1; p.KW = 1; p.pad = 0;
+  p.Cinp = Cin;
+  return launch_conv<ALOAD_DENSE>(p, PIPNET_EPI_DUAL_BIAS_RELU, 9, (hipStream_t)stream);
 }
 
 extern "C" int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y,

@@ -39,6 +39,9 @@ struct ConvParams {
   const float* scale;  // [N] layer scale (EPI_F32_RESID)
   const float* R32;    // fp32 residual [M][ldr] (EPI_F32_RESID), may alias Cf
   float* Cf;           // fp32 output [M][ldc] (EPI_F32_BIAS / EPI_F32_RESID)
+  bf16* C2;            // EPI_DUAL_BIAS_RELU: columns >= nsplit go here (relu), [M][ldc2]
+  int64_t ldc2;
+  int nsplit;
   int M, N, K, Kv;
   int H, Wd, Cin, OH, OW, stride, KW, pad;
   int Cinp;            // physical channels per pixel of A (= Cin, or 2 seg for split planes)
@@ -927,6 +930,11 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     float* wt = reinterpret_cast<float*>(smem + ppp::OFF_EPI) + wid * 16 * 64;
     const int c8 = lane & 7;
     const int n = cn0 + wc * 64 + 8 * c8;
+    // EPI_DUAL_BIAS_RELU: a whole 256-wide tile lies on one side of nsplit (both % 256 == 0)
+    const bool second = EPI == PIPNET_EPI_DUAL_BIAS_RELU && cn0 >= p.nsplit;
+    bf16* const cout = second ? p.C2 : p.C;
+    const int64_t ldo = second ? p.ldc2 : p.ldc;
+    const int no = second ? n - p.nsplit : n;
     f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
     if (EPI != PIPNET_EPI_NONE && p.bias) {
       b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
@@ -966,7 +974,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
             x1[e] += (float)rr[r * 2 + it][4 + e];
           }
         }
-        if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
+        if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU || second) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             x0[e] = fmaxf(x0[e], 0.f);
@@ -980,7 +988,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
           o[4 + e] = (bf16)x1[e];
         }
         const int m = min(cm0 + wr * 128 + r * 16 + row, p.M - 1);
-        *reinterpret_cast<bf16x8v*>(p.C + (int64_t)m * p.ldc + n) = o;
+        *reinterpret_cast<bf16x8v*>(cout + (int64_t)m * ldo + no) = o;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }

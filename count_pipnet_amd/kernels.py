@@ -344,6 +344,23 @@ def nchw_to_nhwc_bf16(x: Tensor, cpad: int) -> Tensor:
     return y
 
 
+def conv1x1_bf16_dual(x: Tensor, w_packed: Tensor, bias: Tensor, n1: int, n2: int) -> Tuple[Tensor, Tensor]:
+    """Two 1x1 stride-1 bf16 convs over one NHWC input in one launch (pipnet_conv1x1_bf16_dual):
+    w_packed = the two packed weights stacked [n1 + n2, Kp], bias [n1 + n2] fp32 ->
+    (x W1^T + b1, relu(x W2^T + b2)), each bit-equal to its own pipnet_conv2d_nhwc_bf16."""
+    _chk_bf(x, "conv input")
+    b, h, w, cin = x.shape
+    if tuple(w_packed.shape[:1]) != (n1 + n2,) or bias.numel() != n1 + n2 or n1 % 256 or n2 % 256:
+        raise RuntimeError(f"conv1x1_bf16_dual: weights {tuple(w_packed.shape)}, n1 {n1}, n2 {n2}")
+    y1 = torch.empty((b, h, w, n1), device=x.device, dtype=torch.bfloat16)
+    y2 = torch.empty((b, h, w, n2), device=x.device, dtype=torch.bfloat16)
+    m = b * h * w
+    _launch("pipnet_bf16::conv_bf16_ppp_kernel<12>", 2.0 * m * (n1 + n2) * cin,
+            lambda: _lib.call("pipnet_conv1x1_bf16_dual", x.data_ptr(), m, cin, w_packed.data_ptr(), bias.data_ptr(),
+                              n1, y1.data_ptr(), n2, y2.data_ptr(), _stream(x)))
+    return y1, y2
+
+
 def nchw_to_s2d_bf16(x: Tensor) -> Tensor:
     """[B,3,H,W] fp32 -> [B, (H-1)//2 + 4, (W-1)//2 + 4, 16] bf16 space-to-depth stem input
     (pipnet_nchw_to_s2d_bf16): the k7 s2 p3 ResNet stem becomes a 4x4 stride-1 conv over it."""

@@ -80,8 +80,40 @@ def _conv_bn(cache, key, conv, bn, x, epilogue, r=None, cpad=None):
     return K.conv2d_nhwc(x, w, b, conv.stride[0], conv.padding[0], epilogue, r)
 
 
+DUAL_1X1 = True      # tools / A-B runs may switch the dual downsample + conv1 launch off
+
+
+def _dual_ok(blk, h) -> bool:
+    """A first Bottleneck whose downsample and conv1 are both 1x1 stride-1 convs over h with
+    Cout % 256 == 0 (C3's layer3 / layer4 at stride 1): one launch for both (the input read once)."""
+    if not DUAL_1X1 or h.dtype != torch.bfloat16 or blk.downsample is None or len(blk.downsample) != 2:
+        return False
+    ds, c1 = blk.downsample[0], blk.conv1
+    return all(isinstance(c, nn.Conv2d) and c.kernel_size == (1, 1) and c.stride == (1, 1) and c.padding == (0, 0)
+               and c.groups == 1 and c.out_channels % 256 == 0 for c in (ds, c1)) and isinstance(blk.downsample[1],
+                                                                                                   nn.BatchNorm2d)
+
+
+def _dual_weights(cache, key, blk):
+    """Folded + packed downsample and conv1 weights stacked [N_ds + N_c1, Kp], biases stacked."""
+    wd, bd = _fold(cache, key + ".ds", blk.downsample[0], blk.downsample[1], bf16=True)
+    w1, b1 = _fold(cache, key + ".c1", blk.conv1, blk.bn1, bf16=True)
+    ck = (key + ".dual", str(wd.device))
+    ent = cache.get(ck)
+    if ent is None or ent[0][0] is not wd or ent[0][1] is not w1:
+        with torch.no_grad():
+            ent = ((wd, w1), (torch.cat([wd, w1]).contiguous(), torch.cat([bd, b1]).contiguous()))
+        cache[ck] = ent
+    return ent[1][0], ent[1][1], wd.shape[0], w1.shape[0]
+
+
 def _bottleneck(cache, key, blk, h):
     from .resnet_features import BasicBlock, Bottleneck
+    if isinstance(blk, Bottleneck) and _dual_ok(blk, h):
+        w, b, nd, n1 = _dual_weights(cache, key, blk)
+        idt, t = K.conv1x1_bf16_dual(h, w, b, nd, n1)
+        t = _conv_bn(cache, key + ".c2", blk.conv2, blk.bn2, t, _lib.EPI_BIAS_RELU)
+        return _conv_bn(cache, key + ".c3", blk.conv3, blk.bn3, t, _lib.EPI_BIAS_RESID_RELU, r=idt)
     if blk.downsample is not None:
         ds_conv, ds_bn = blk.downsample[0], blk.downsample[1]
         idt = _conv_bn(cache, key + ".ds", ds_conv, ds_bn, h, _lib.EPI_BIAS)

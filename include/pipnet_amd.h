@@ -45,6 +45,7 @@ extern "C" {
 #define PIPNET_EPI_S3_GELU 9         /* g = gelu_erf(A W^T + b) stored as split planes [hi|lo] bf16    */
 #define PIPNET_EPI_F32_BIAS 10       /* C = A W^T + b, fp32                                            */
 #define PIPNET_EPI_F32_RESID 11      /* C = R + s * (A W^T + b), fp32 C and R (R may alias C)          */
+#define PIPNET_EPI_DUAL_BIAS_RELU 12 /* columns < N1: C = A W^T + b; columns >= N1: C2 = relu(A W^T + b) (bf16 1x1 convs, pipnet_conv1x1_bf16_dual) */
 
 /* ABI version: bumped whenever an exported signature changes.  2: pipnet_wgrad_conv_f32 gained
  * its `pad` argument (round 2); a caller built against version 1 must not bind this library. */
@@ -203,6 +204,15 @@ int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k,
 
 /* fp32 NCHW -> bf16 NHWC (round to nearest even), channels zero-padded to Cpad (% 8 == 0). */
 int pipnet_nchw_to_nhwc_bf16(const float* x, int B, int C, int H, int W, int Cpad, void* y, void* stream);
+
+/* Two 1x1 stride-1 bf16 convs over the same input in one launch (a ResNet stage's first
+ * Bottleneck: the downsample conv + BN and conv1 + BN + ReLU, resnet_features.py:95-117):
+ * w_packed = [N1 + N2, Kp] (rows 0..N1-1 the first conv), bias [N1 + N2];
+ *   y1[M,N1] = x W1^T + b1,   y2[M,N2] = relu(x W2^T + b2).
+ * x: [M, Cin] bf16 (NHWC pixels), N1 % 256 == 0, N2 % 256 == 0.  Each output equals the
+ * single-conv launch bit for bit (same tile, same K order); the input is read once. */
+int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias, int N1,
+                             void* y1, int N2, void* y2, void* stream);
 
 /* ResNet stem input for a 3-channel k7 s2 p3 conv run as a 4x4 stride-1 conv: fp32 NCHW [B,3,H,W]
  * -> bf16 2x2 space-to-depth image [B, SH, SW, 16], SH = (H-1)/2 + 4, SW = (W-1)/2 + 4,

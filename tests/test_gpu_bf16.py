@@ -241,6 +241,21 @@ def test_stem_s2d_bf16(gpu, h, w):
     assert torch.all(err <= 1e-2 * (1 + ref.abs())), err.max()      # bf16 output rounding (2^-8)
 
 
+@pytest.mark.parametrize("m,cin,n1,n2", [(2 * 28 * 28, 512, 1024, 256), (3 * 17 * 11, 1024, 2048, 512), (300, 256, 256, 256)])
+def test_conv1x1_bf16_dual_matches_single(gpu, m, cin, n1, n2):
+    """The dual 1x1 launch (a first Bottleneck's downsample + conv1 over one input read) gives
+    each output bit for bit as its own persistent-tile conv."""
+    g = torch.Generator().manual_seed(m + n1)
+    x = torch.randn(1, m, 1, cin, generator=g).to(torch.bfloat16).to(gpu)
+    w1 = K.pack_conv_weight_bf16((torch.randn(n1, 1, 1, cin, generator=g) * 0.05).to(gpu))
+    w2 = K.pack_conv_weight_bf16((torch.randn(n2, 1, 1, cin, generator=g) * 0.05).to(gpu))
+    b1, b2 = torch.randn(n1, generator=g).to(gpu), torch.randn(n2, generator=g).to(gpu)
+    y1, y2 = K.conv1x1_bf16_dual(x, torch.cat([w1, w2]), torch.cat([b1, b2]), n1, n2)
+    r1 = K.conv2d_nhwc_bf16(x, w1, 1, 1, b1, 1, 0, _lib.EPI_BIAS)
+    r2 = K.conv2d_nhwc_bf16(x, w2, 1, 1, b2, 1, 0, _lib.EPI_BIAS_RELU)
+    assert torch.equal(y1, r1) and torch.equal(y2, r2)
+
+
 def _c3_bf16(gpu, num_features=0):
     from golden_util import golden_args, golden_inputs, golden_state_dict, load_golden
     from model_util import build_model

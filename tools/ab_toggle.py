@@ -1,0 +1,60 @@
+"""Interleaved A/B of a module-level switch of the HIP path on one BASELINE config, in one process
+(cdna_hip_programming.md rule 24): rounds of (off, on) timings of net(xs, inference=True).
+
+    python tools/ab_toggle.py <module>.<FLAG> <config> [--rounds 5] [--steps 10]
+e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3"""
+import argparse
+import importlib
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import bench_configs as bc  # noqa: E402
+from count_pipnet_amd.synthetic import synth_images  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("flag")
+    ap.add_argument("config")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    a = ap.parse_args()
+    modname, attr = a.flag.rsplit(".", 1)
+    mod = importlib.import_module(modname)
+    dev = torch.device("cuda:0")
+    cfg = bc.CONFIGS[a.config]
+    net = bc.make(cfg, dev)
+    xs = synth_images(cfg["batch"], cfg["size"], seed=1).to(dev)
+    res = {False: [], True: []}
+    outs = {}
+    with torch.no_grad():
+        for r in range(a.rounds):
+            for val in (False, True):
+                setattr(mod, attr, val)
+                for _ in range(2):
+                    o = net(xs, inference=True)
+                torch.cuda.synchronize()
+                if r == 0:
+                    outs[val] = [t.float().clone() for t in o]
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.steps):
+                    net(xs, inference=True)
+                e1.record()
+                torch.cuda.synchronize()
+                res[val].append(e0.elapsed_time(e1) / a.steps)
+    same = all(torch.equal(x, y) for x, y in zip(outs[False], outs[True]))
+    for val in (False, True):
+        ms = sorted(res[val])
+        print(json.dumps({"flag": a.flag, "value": val, "config": a.config, "ms_median": ms[len(ms) // 2],
+                          "ms_min": ms[0], "img_s_median": cfg["batch"] / ms[len(ms) // 2] * 1e3}))
+    print(json.dumps({"outputs_bitwise_equal": same}))
+
+
+if __name__ == "__main__":
+    main()
