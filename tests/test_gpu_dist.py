@@ -253,3 +253,76 @@ def test_c4_per_rank_shard_vs_oracle(gpu, tmp_path):
     # the decisive-argmax comparison is not vacuous on this workload
     srt = np.sort(r_out_inf.numpy(), axis=1)
     assert ((srt[:, -1] - srt[:, -2]) > 2e-3 * np.maximum(1, np.abs(srt)).max(axis=1)).sum() >= 32
+
+
+def _count_worker(rank, world, port, batch, q):
+    """BASELINE configs[4]'s layout: the C5 CountPIPNet (bilinear, hard Gumbel head, 2048
+    prototypes) with each rank passing its own shard (bench.py's call pattern) and the Exp(1)
+    draw of its images injected; the gathered counts / logits and the rank's proto shard vs
+    the single-process forward of the whole batch with the whole draw (bitwise)."""
+    import sys
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    sys.path.insert(0, TESTS)
+    sys.path.insert(0, os.path.dirname(TESTS))
+    import torch.distributed as dist
+    res = {"rank": rank}
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from count_pipnet_amd.dist import ShardedInference, shard_sizes
+        from count_pipnet_amd.synthetic import synth_exponential, synth_images
+        from golden_util import load_golden
+        from model_util import build_model
+        meta, _ = load_golden("c5_count_bilinear_2048")
+        net = build_model(meta).to(dev)
+        size = meta["case"]["size"]
+        xs = synth_images(batch, size, seed=55).to(dev)
+        p, h, w = 2048, size // 8, size // 8                  # prototypes, proto grid (16 x 16 at 128^2)
+        noise = synth_exponential((batch, p, h, w), seed=56).to(dev)
+        sizes = shard_sizes(batch, world)
+        start = sum(sizes[:rank])
+        wrapped = ShardedInference(net)
+        with torch.no_grad():
+            net._add_on[-1].exp_noise = noise
+            r_proto, r_counts, r_out = net(xs, inference=True)
+            net._add_on[-1].exp_noise = noise[start:start + sizes[rank]]
+            proto, counts, out = wrapped(xs[start:start + sizes[rank]].contiguous(), inference=True,
+                                         global_batch=False, sizes=sizes)
+        torch.cuda.synchronize()
+        res.update(grid=tuple(r_proto.shape) == (batch, p, h, w),
+                   proto=torch.equal(proto, r_proto[start:start + sizes[rank]]),
+                   counts=torch.equal(counts, r_counts), out=torch.equal(out, r_out),
+                   shapes=tuple(counts.shape) == (batch, p) and tuple(out.shape) == (batch, r_out.shape[1]),
+                   backend=dist.get_backend(), module=wrapped.module is net, device=str(out.device))
+    except Exception as e:
+        res["error"] = repr(e)
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    q.put(res)
+
+
+def test_c5_count_sharded_gloo_world4(gpu):
+    """BASELINE configs[4] shards its batch over 4 GPUs: the C5 CountPIPNet through a world-4
+    gloo group on cuda:0 (8 images -> 2 per rank), gathered counts / logits bitwise equal to
+    the single-process forward on every rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world, batch = 4, 8
+    procs = [ctx.Process(target=_count_worker, args=(r, world, port, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r = q.get(timeout=300)
+            res[r["rank"]] = r
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    _assert_all(res, world, "gloo")
