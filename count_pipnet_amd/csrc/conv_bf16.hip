@@ -75,6 +75,13 @@ bool is_s3_epi(int epi) {
 // 3x3 / stride 1 / pad 1 convs with N >= 256 whose halo fits the kernel's 320 LDS rows
 // (256 + 2W + 2): the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer
 // choice, never M.
+// 3x3 / stride 1 / pad 1 convs with N = 64 (layer1 conv2): the N = 64 LDS-halo tile (11) -- a
+// per-layer choice, never M.
+bool halo64_ok(const ConvParams& p, int epi) {
+  return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
+         p.seg == 0 && p.Cin == 64 && p.Wd <= 63 && p.N == 64 && !is_s3_epi(epi);
+}
+
 bool halo_ok(const ConvParams& p, int epi) {
   return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
          p.seg == 0 && p.Cin % 64 == 0 && p.Wd <= 31 && p.N >= 256 && !is_s3_epi(epi);
@@ -82,20 +89,45 @@ bool halo_ok(const ConvParams& p, int epi) {
 // B fragments of 16 columns per wave.  Only the 256-wide tile is dispatched: the 64 / 128-wide
 // instantiations (4 / 8 MFMAs per phase) measured slower than tile 6 on layer1 conv2 (125 vs
 // 88 us) and +5 % on layer2 conv2 (profiles/r02/conv_bf16_halo_narrow.log).
+// the N = 64 halo tile (11), bitwise tile 6: layer1 conv2 52 -> 28 us at 64 images, 88 -> 46 us at 128
+// (profiles/r03/conv_bf16_n64.log)
+#ifndef H64_AUTO
+#define H64_AUTO 1
+#endif
 int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
   const bool hk = ALOAD == ALOAD_CONV && halo_ok(p, epi);
+  const bool h64 = ALOAD == ALOAD_CONV && halo64_ok(p, epi);
   // 1x1 convs with N % 256 == 0: the persistent ping-pong tile (9), same K order as tile 5
   const bool pk = ALOAD == ALOAD_DENSE && pp_ok && p.N % 256 == 0 && !is_s3_epi(epi);
   if (v < 0) {
     v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv > 0 ? p.Kv : p.K);
     if (hk) v = 8;
+    else if (h64 && H64_AUTO) v = 11;
     else if (v == 5 && pk) v = 9;
   }
-  if (v > 9 || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
+  if (v > 11 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
+  if (v == 11) {                                 // N = 64 3x3 on the LDS input halo
+    p.nt = 1;
+    p.mt = (p.M + 255) / 256;
+    const dim3 grid(p.mt);
+    switch (epi) {
+      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_NONE>), grid, dim3(256), 0, s, p); break;
+      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS>), grid, dim3(256), 0, s, p); break;
+      case PIPNET_EPI_BIAS_RELU:
+        hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(256), 0, s, p);
+        break;
+      case PIPNET_EPI_BIAS_RESID_RELU:
+        hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(256), 0, s, p);
+        break;
+      default: return PIPNET_ERR_ARG;
+    }
+    PIPNET_CHECK_LAUNCH();
+    return PIPNET_OK;
+  }
   if (v == 9) {                                  // persistent 256 x 256 ping-pong (1x1, N % 256 == 0)
     p.nt = p.N / 256;
     p.mt = (p.M + 255) / 256;

@@ -230,9 +230,10 @@ def _chk_bf(t: Tensor, what: str) -> None:
 
 
 def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int = 0, halo_ok: bool = False,
-                   ppp_ok: bool = False) -> int:
+                   ppp_ok: bool = False, halo64_ok: bool = False) -> int:
     """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
+    11 = 3x3 stride-1 pad-1 Cin = N = 64 convs (W <= 63) on an LDS input halo (tile 6's arithmetic),
     8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31, N >= 256),
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 / 8 / 9 on
@@ -249,6 +250,8 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
         return 5 if n >= 256 else m128
     if halo_ok:
         return 8
+    if halo64_ok:
+        return 11
     short_k = 0 < kv <= 64                  # layer1 conv3 / downsample (K = 64): 2-workgroup tiles
     if n >= 256 and pp_ok and not short_k:
         return 9 if ppp_ok else 5
@@ -265,9 +268,12 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
 
 
 def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True,
-                          s3: bool = False, kv: int = 0, halo_ok: bool = False, ppp_ok: bool = False) -> str:
+                          s3: bool = False, kv: int = 0, halo_ok: bool = False, ppp_ok: bool = False,
+                          halo64_ok: bool = False) -> str:
     """rocprof name of the bf16 conv instantiation."""
-    t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok) if tile < 0 else tile
+    t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok, halo64_ok) if tile < 0 else tile
+    if t == 11:
+        return f"pipnet_bf16::conv3x3_bf16_n64_kernel<{epilogue}>"
     if t == 9:
         return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}>"
     if t == 8:
@@ -292,13 +298,18 @@ def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
     return out
 
 
+# Tile 11 (3x3 Cin = N = 64 on the LDS input halo) for automatic launches; False = tile 6, bitwise
+# the same outputs (in-process A/B: tools/ab_toggle.py count_pipnet_amd.kernels.CONV3X3_N64_HALO c3)
+CONV3X3_N64_HALO = True
+
+
 def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Optional[Tensor], stride: int,
                      pad: int, epilogue: int = _lib.EPI_BIAS, r: Optional[Tensor] = None, tile: int = -1) -> Tensor:
     """NHWC bf16 implicit-GEMM convolution; w_packed from pack_conv_weight_bf16; bias fp32;
     tile -1 = automatic, 0 = 64x128 (32-deep K, 4 stages), 1/2 = 128x128 / 256x256 (64-deep K,
     2 stages), 3/4 = 256x256 / 128x128 (32-deep K, 4 stages), 5 = 256x256 ping-pong, 6 = 256x64,
     8 = ping-pong with the LDS input halo (3x3 stride-1 pad-1 only), 9 = persistent ping-pong
-    (1x1 stride-1, N % 256 == 0)."""
+    (1x1 stride-1, N % 256 == 0), 11 = 3x3 stride-1 pad-1 N = 64 on an LDS input halo."""
     _chk_bf(x, "conv input")
     _chk_bf(w_packed, "conv weight")
     if r is not None:
@@ -319,7 +330,12 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
                and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     ppp_ok = (aload == 0 and pp_ok and cout % 256 == 0
               and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok),
+    halo64_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == 64 and w <= 63 and cout == 64
+                 and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
+    if halo64_ok and tile < 0 and not CONV3X3_N64_HALO:
+        tile = 6                            # the same arithmetic on the generic N = 64 tile
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok,
+                                  halo64_ok=halo64_ok),
             2.0 * m * cout * k,
             lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
                               _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), tile,

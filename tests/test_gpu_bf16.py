@@ -256,6 +256,51 @@ def test_conv1x1_bf16_dual_matches_single(gpu, m, cin, n1, n2):
     assert torch.equal(y1, r1) and torch.equal(y2, r2)
 
 
+@pytest.mark.parametrize("b,h,w,epi", [(2, 56, 56, _lib.EPI_BIAS_RELU), (3, 17, 13, _lib.EPI_BIAS_RELU),
+                                      (1, 9, 63, _lib.EPI_BIAS), (2, 11, 7, _lib.EPI_BIAS_RESID_RELU),
+                                      (1, 5, 5, _lib.EPI_NONE), (5, 1, 1, _lib.EPI_BIAS_RELU)])
+def test_conv3x3_n64_halo(gpu, b, h, w, epi):
+    """Tile 11 (3x3 s1 p1, Cin = N = 64, LDS input halo) is bitwise equal to tile 6 -- same
+    MFMA shape, same K order, same epilogue -- so choosing it changes no output bit; also
+    against the fp64 conv of the same bf16 values (bf16 output rounding), image-boundary taps,
+    ragged M (rows past the last 256-pixel tile), every epilogue; and batch invariance (image 1
+    alone == image 1 in the batch)."""
+    cin = 64
+    g = torch.Generator().manual_seed(cin + h * w + b)
+    x = torch.randn(b, h, w, cin, generator=g).to(torch.bfloat16)
+    wt = (torch.randn(64, 3, 3, cin, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(64, generator=g)
+    r = torch.randn(b, h, w, 64, generator=g).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
+    wp = K.pack_conv_weight_bf16(wt.float().to(gpu))
+    run = lambda xx, rr, t: K.conv2d_nhwc_bf16(xx.to(gpu), wp, 3, 3, bias.to(gpu), 1, 1, epi,  # noqa: E731
+                                               None if rr is None else rr.to(gpu), tile=t)
+    out11 = run(x, r, 11)
+    assert torch.equal(out11, run(x, r, 6))
+    out = out11.double().cpu()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), wt.double().permute(0, 3, 1, 2), padding=1)
+    if epi != _lib.EPI_NONE:
+        ref = ref + bias.double().view(1, -1, 1, 1)
+    ref = ref.permute(0, 2, 3, 1)
+    if r is not None:
+        ref = ref + r.double()
+    if epi in (_lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU):
+        ref = torch.relu(ref)
+    err = (out - ref).abs()
+    assert torch.all(err <= 1e-2 * (1 + ref.abs())), err.max()
+    if b > 1:
+        one = run(x[1:2], None if r is None else r[1:2], 11).cpu()
+        assert torch.equal(one[0], out11[1].cpu())
+
+
+def test_conv3x3_n64_halo_rejects(gpu):
+    """Tile 11 forced on a layer outside its scope (Cin != 64, W > 63) is an argument error."""
+    for cin, w in ((32, 8), (64, 64)):
+        x = torch.zeros(1, 4, w, cin, dtype=torch.bfloat16, device=gpu)
+        wp = K.pack_conv_weight_bf16(torch.zeros(64, 3, 3, cin, device=gpu))
+        with pytest.raises(RuntimeError):
+            K.conv2d_nhwc_bf16(x, wp, 3, 3, None, 1, 1, _lib.EPI_NONE, None, tile=11)
+
+
 def _c3_bf16(gpu, num_features=0):
     from golden_util import golden_args, golden_inputs, golden_state_dict, load_golden
     from model_util import build_model
