@@ -140,6 +140,8 @@ def test_conv_bf16_halo(gpu, b, cin, cout, h, w, epi):
     (70000, 512, 512, _lib.EPI_BIAS_RESID_RELU),    # 548 tiles: several tiles per persistent workgroup
     (70000, 256, 1024, _lib.EPI_BIAS),              # 1096 tiles, 8 K-tiles
     (9000, 1024, 256, _lib.EPI_NONE),               # long K
+    (12544, 256, 1024, _lib.EPI_BIAS_RESID_RELU),   # layer3 conv3 + identity (16 images)
+    (3337, 512, 2048, _lib.EPI_BIAS_RESID_RELU),    # layer4 conv3 + identity, ragged M
 ])
 def test_conv_bf16_persistent_pp(gpu, m, cin, cout, epi):
     """Persistent ping-pong tile (tile 9, 1x1 convs with N % 256 == 0): same K order as the
