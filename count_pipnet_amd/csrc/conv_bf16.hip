@@ -75,11 +75,13 @@ bool is_s3_epi(int epi) {
 // 3x3 / stride 1 / pad 1 convs with N >= 256 whose halo fits the kernel's 320 LDS rows
 // (256 + 2W + 2): the LDS-halo ping-pong kernel (tile 8) replaces tile 5 -- a per-layer
 // choice, never M.
-// 3x3 / stride 1 / pad 1 convs with N = 64 (layer1 conv2): the N = 64 LDS-halo tile (11) -- a
-// per-layer choice, never M.
+// 3x3 / stride 1 / pad 1 convs with Cin = N = 64 (layer1 conv2, W <= 63) or Cin = N = 128
+// (layer2 conv2, W <= 31): the small-N LDS-halo tile (11) -- a per-layer choice, never M.
 bool halo64_ok(const ConvParams& p, int epi) {
+  const bool shape = (p.Cin == 64 && p.N == 64 && p.Wd <= hsm::Shape<64>::MAX_W) ||
+                     (p.Cin == 128 && p.N == 128 && p.Wd <= hsm::Shape<128>::MAX_W);
   return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
-         p.seg == 0 && p.Cin == 64 && p.Wd <= 63 && p.N == 64 && !is_s3_epi(epi);
+         p.seg == 0 && shape && !is_s3_epi(epi);
 }
 
 bool halo_ok(const ConvParams& p, int epi) {
@@ -110,21 +112,29 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     else if (v == 5 && pk) v = 9;
   }
   if (v > 11 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
-  if (v == 11) {                                 // N = 64 3x3 on the LDS input halo
+  if (v == 11) {                                 // Cin = N = 64 / 128 3x3 on the LDS input halo
+    const int bm = p.N == 64 ? hsm::Shape<64>::BM : hsm::Shape<128>::BM;
     p.nt = 1;
-    p.mt = (p.M + 255) / 256;
+    p.mt = (p.M + bm - 1) / bm;
     const dim3 grid(p.mt);
-    switch (epi) {
-      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_NONE>), grid, dim3(256), 0, s, p); break;
-      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS>), grid, dim3(256), 0, s, p); break;
-      case PIPNET_EPI_BIAS_RELU:
-        hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(256), 0, s, p);
-        break;
-      case PIPNET_EPI_BIAS_RESID_RELU:
-        hipLaunchKernelGGL((conv3x3_bf16_n64_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(256), 0, s, p);
-        break;
-      default: return PIPNET_ERR_ARG;
+#define PIPNET_HSM(CIN)                                                                                  \
+    switch (epi) {                                                                                       \
+      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv3x3_bf16_hsmall_kernel<CIN, PIPNET_EPI_NONE>), grid, dim3(256), 0, s, p); break; \
+      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv3x3_bf16_hsmall_kernel<CIN, PIPNET_EPI_BIAS>), grid, dim3(256), 0, s, p); break; \
+      case PIPNET_EPI_BIAS_RELU:                                                                         \
+        hipLaunchKernelGGL((conv3x3_bf16_hsmall_kernel<CIN, PIPNET_EPI_BIAS_RELU>), grid, dim3(256), 0, s, p); \
+        break;                                                                                           \
+      case PIPNET_EPI_BIAS_RESID_RELU:                                                                   \
+        hipLaunchKernelGGL((conv3x3_bf16_hsmall_kernel<CIN, PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(256), 0, s, p); \
+        break;                                                                                           \
+      default: return PIPNET_ERR_ARG;                                                                    \
     }
+    if (p.N == 64) {
+      PIPNET_HSM(64)
+    } else {
+      PIPNET_HSM(128)
+    }
+#undef PIPNET_HSM
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }

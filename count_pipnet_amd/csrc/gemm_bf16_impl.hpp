@@ -1233,57 +1233,73 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
 }
 
 // ======================================================================================
-// 3x3 / stride 1 / pad 1 convolutions with Cin = N = 64 (ResNet layer1 conv2) on an LDS input halo.
+// 3x3 / stride 1 / pad 1 convolutions with Cin = N = 64 (ResNet layer1 conv2, tile M 256) or
+// Cin = N = 128 (layer2 conv2, tile M 128) on an LDS input halo -- "tile 11".
 //
-// The generic N = 64 tile (tile 6, 256 x 64) walks K = 9 x 64 as 32-deep K-tiles and brings
-// every tap's 256 x 32 A block through the LDS-DMA path -- the input 9 times -- while a K-tile
-// holds only 4 MFMAs per wave: at ~300 TF/s it is DMA-path bound.  Here a 256-pixel tile stages
-// the linear pixel range [m0 - W - 1, m0 + 256 + W + 1) once, all 64 channels (<= 384 rows of
-// 128 B, 48 KiB), and streams the weights one tap (64 x 64, 8 KiB) at a time through a 3-slot
-// ring, tap t + 2 in flight while tap t is multiplied: 72 KiB, two workgroups per CU.
-// Arithmetic is tile 6's, bit for bit: MFMA 32x32x16, each of the 4 waves owning 64 pixels x
-// 64 columns (2 x 2 blocks), K walked in tile 6's order -- tap-major, then 32-channel chunk,
-// then the chunk's two k-steps, with half-wave h supplying channels 8 (2 h + q) .. +7 of step
-// q -- and the same epilogue, so switching tiles changes no output bit (tests/test_gpu_bf16.py).
+// The generic tiles for these layers (tile 6, 256 x 64; tile 4, 128 x 128) walk K = 9 Cin as
+// 32-deep K-tiles and bring every tap's A block through the LDS-DMA path -- the input 9 times --
+// with 4 / 8 MFMAs per wave per K-tile: DMA-path bound at ~300 / ~430 TF/s.  Here a BM-pixel
+// tile stages the linear pixel range [m0 - W - 1, m0 + BM + W + 1) once, all Cin channels
+// (48 KiB: <= 384 rows of 128 B / <= 192 rows of 256 B), and streams the weights through a
+// 3-slot ring of 8 KiB K-tiles (N x KT: one tap at N = 64, one 32-channel chunk of a tap at
+// N = 128), K-tile k + 2 in flight while k is multiplied: 72 KiB, two workgroups per CU.
+// Arithmetic is the generic tiles', bit for bit: MFMA 32x32x16, each of the 4 waves owning 64
+// pixels x 64 columns (2 x 2 blocks), K walked in their order -- tap-major, then 32-channel
+// chunk, then the chunk's two k-steps, half-wave h supplying channels 8 (2 h + q) .. +7 of step
+// q -- and the same epilogue, so choosing this tile changes no output bit (tests/test_gpu_bf16.py).
 // Taps that leave the image read a 256-B zero block at the same bank slot (9-bit mask per
-// fragment row), the zeros tile 6 reads there.  Rows (halo pixels and weight rows alike) hold
-// 16-B chunk k at k ^ ((r >> 1) & 7): every ds_read_b128 lane group then covers 16 consecutive
-// rows mod 16 and so 16 distinct bank slots, at any tap's row offset.
-// Requirements: KH = KW = 3, stride 1, pad 1, Cin = N = 64, W <= 63, no seg.
+// fragment row), the zeros the generic tiles read there.  Rows of RB bytes (halo pixels, weight
+// rows) hold 16-B chunk k at k ^ ((r >> log2(256 / RB)) & (RB / 16 - 1)): every ds_read_b128
+// lane group covers 16 consecutive rows mod 16 and so 16 distinct bank slots, at any tap offset.
+// Requirements: KH = KW = 3, stride 1, pad 1, Cin = N in {64, 128}, W <= 63 / 31, no seg.
 // ======================================================================================
-namespace h64 {
-constexpr int NT = 256, BM = 256, BN = 64;
-constexpr int ROWB = 128;                             // 64 bf16 channels per LDS row
-constexpr int HALO_ROWS = 384;                        // 256 + 2 W + 2 for W <= 63
-constexpr int HALO_BYTES = HALO_ROWS * ROWB;          // 48 KiB
-constexpr int TAP_BYTES = BN * ROWB;                  // 8 KiB: one tap's 64 x 64 weights
-constexpr int NSLOT = 3;
-constexpr int OFF_B = HALO_BYTES, OFF_ZERO = OFF_B + NSLOT * TAP_BYTES;
+namespace hsm {
+constexpr int NT = 256, NSLOT = 3, SLOT_BYTES = 8192, HALO_BYTES = 48 * 1024;
+constexpr int OFF_B = HALO_BYTES, OFF_ZERO = OFF_B + NSLOT * SLOT_BYTES;
 constexpr int SMEM = OFF_ZERO + 256;
 constexpr int EPI_LD = 68;                            // epilogue fp32 rows: 64 + 4 pad
 static_assert(4 * 32 * EPI_LD * 4 <= SMEM, "epilogue re-lay fits");
 static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
-PIPNET_DEV int sw(int r) { return (r >> 1) & 7; }
-}  // namespace h64
+template <int CIN>
+struct Shape {
+  static constexpr int BN = CIN, BM = CIN == 64 ? 256 : 128;
+  static constexpr int WN = BN / 64, WM = 4 / WN;     // waves: WM x WN, 64 x 64 each
+  static constexpr int KT = SLOT_BYTES / (2 * BN);    // channels per weight K-tile (64 / 32)
+  static constexpr int NKT = 9 * CIN / KT;            // K-tiles per tile (9 / 36)
+  static constexpr int RB = 2 * CIN, WB = 2 * KT;     // halo / weight row bytes
+  static constexpr int HALO_ROWS = HALO_BYTES / RB;   // 384 / 192
+  static constexpr int MAX_W = (HALO_ROWS - BM - 2) / 2;
+  static_assert(WM * 64 == BM, "wave grid");
+};
+// 16-B slot swizzle of a row of RB bytes
+template <int RB>
+PIPNET_DEV int sw(int r) {
+  return RB == 256 ? (r & 15) : RB == 128 ? ((r >> 1) & 7) : ((r >> 2) & 3);
+}
+}  // namespace hsm
 
-template <int EPI>
-__global__ __launch_bounds__(h64::NT, 2) void conv3x3_bf16_n64_kernel(ConvParams p) {
-  using namespace h64;
+template <int CIN, int EPI>
+__global__ __launch_bounds__(hsm::NT, 2) void conv3x3_bf16_hsmall_kernel(ConvParams p) {
+  using namespace hsm;
+  using S = Shape<CIN>;
+  constexpr int BM = S::BM, RB = S::RB, WB = S::WB, KT = S::KT, NKT = S::NKT;
   __shared__ __attribute__((aligned(256))) unsigned char smem[SMEM];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
+  const int wm = wid / S::WN, wn = wid % S::WN;
   const int nwg = (p.M + BM - 1) / BM;
   const int m0 = xcd_remap(blockIdx.x, nwg) * BM;
   const int W = p.Wd, HW = p.H * p.Wd;
-  const int npiece = ((BM + 2 * W + 2) + 7) >> 3;       // 1-KiB halo pieces (8 rows) actually used
+  constexpr int HROWS_PC = 1024 / RB;                   // halo rows per 1-KiB DMA piece
+  const int npiece = ((BM + 2 * W + 2) + HROWS_PC - 1) / HROWS_PC;
 
-  // ---- this lane's 2 fragment pixels (64 wid + 32 i + (lane & 31)): 9-bit tap masks ----
+  // ---- this lane's 2 fragment pixels (64 wm + 32 i + (lane & 31)): 9-bit tap masks ----
   const int lr = lane & 31, lh = lane >> 5;
   unsigned vmask[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int m = m0 + 64 * wid + 32 * i + lr;
+    const int m = m0 + 64 * wm + 32 * i + lr;
     unsigned mk = 0;
     if (m < p.M) {
       const int rr = m % HW;
@@ -1298,26 +1314,31 @@ __global__ __launch_bounds__(h64::NT, 2) void conv3x3_bf16_n64_kernel(ConvParams
   }
   if (tid < 16) *reinterpret_cast<u32x4*>(smem + OFF_ZERO + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 
-  // ---- LDS-DMA: a 1-KiB piece = 8 rows x 8 chunks; lane -> row lane >> 3, slot lane & 7 ----
-  const int drow = lane >> 3, dslot = lane & 7;
+  // ---- LDS-DMA: 1-KiB pieces, lane -> (row, 16-B slot) of a piece of RB- / WB-byte rows ----
   auto dma = [&](const bf16* src, int off) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(smem + off), 16, 0, 0);
   };
-  for (int pc = wid; pc < npiece; pc += 4) {
-    const int r = 8 * pc + drow;
-    const int pix = min(max(m0 - W - 1 + r, 0), p.M - 1);
-    dma(p.A + (int64_t)pix * p.Cinp + 8 * (dslot ^ sw(r)), pc * 1024);
+  {
+    const int drow = lane / (RB / 16), dslot = lane % (RB / 16);
+    for (int pc = wid; pc < npiece; pc += 4) {
+      const int r = HROWS_PC * pc + drow;
+      const int pix = min(max(m0 - W - 1 + r, 0), p.M - 1);
+      dma(p.A + (int64_t)pix * p.Cinp + 8 * (dslot ^ sw<RB>(r)), pc * 1024);
+    }
   }
-  auto stage_tap = [&](int t) {                          // 8 pieces: this wave's wid, wid + 4
+  const int wrow = lane / (WB / 16), wslot = lane % (WB / 16);
+  auto stage_k = [&](int kt) {                          // 8 pieces: this wave's wid, wid + 4
+    const int t = kt / (CIN / KT), c0 = (kt % (CIN / KT)) * KT;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int pc = wid + 4 * h, n = 8 * pc + drow;
-      dma(p.W + (int64_t)n * p.K + t * 64 + 8 * (dslot ^ sw(n)), OFF_B + (t % NSLOT) * TAP_BYTES + pc * 1024);
+      const int pc = wid + 4 * h, n = (1024 / WB) * pc + wrow;
+      dma(p.W + (int64_t)n * p.K + t * CIN + c0 + 8 * (wslot ^ sw<WB>(n)),
+          OFF_B + (kt % NSLOT) * SLOT_BYTES + pc * 1024);
     }
   };
-  stage_tap(0);
-  stage_tap(1);
+  stage_k(0);
+  stage_k(1);
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -1327,47 +1348,54 @@ __global__ __launch_bounds__(h64::NT, 2) void conv3x3_bf16_n64_kernel(ConvParams
 #pragma unroll
       for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
 
-  const int lrow = 64 * wid + lr;                         // halo row of fragment 0 at tap (0, 0)
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    // tap t landed (only tap t + 1's 2 pieces may still fly), every wave done with tap t - 1
-    if (t < 8) wait_dma_barrier<2>();
+  const int lrow = 64 * wm + lr;                          // halo row of fragment 0 at tap (0, 0)
+  auto ktile = [&](int kt) {
+    // K-tile kt landed (only kt + 1's 2 pieces may still fly), every wave done with kt - 1
+    if (kt + 1 < NKT) wait_dma_barrier<2>();
     else wait_dma_barrier<0>();
-    if (t + 2 < 9) stage_tap(t + 2);                      // into the slot tap t - 1 used
+    if (kt + 2 < NKT) stage_k(kt + 2);                    // into the slot K-tile kt - 1 used
+    const int t = kt / (CIN / KT), c0 = (kt % (CIN / KT)) * KT;
     const int ky = t / 3, kx = t - 3 * (t / 3);
-    const unsigned char* bslot = smem + OFF_B + (t % NSLOT) * TAP_BYTES;
+    const unsigned char* bslot = smem + OFF_B + (kt % NSLOT) * SLOT_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {                      // chunk kk >> 1, k-step kk & 1
-      const int cg = 4 * (kk >> 1) + 2 * lh + (kk & 1);   // 16-B channel chunk of this half-wave
+    for (int kk = 0; kk < KT / 16; ++kk) {                // chunk kk >> 1 of the K-tile, k-step kk & 1
+      const int gb = 4 * (kk >> 1) + 2 * lh + (kk & 1);   // 16-B channel group within the K-tile
+      const int ga = c0 / 8 + gb;                         // ... within the pixel's row
       bf16x8 fa[2], fb[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int hr = lrow + 32 * i + ky * W + kx;
-        const int aoff = hr * ROWB + 16 * (cg ^ sw(hr));
+        const int aoff = hr * RB + 16 * (ga ^ sw<RB>(hr));
         const unsigned char* ptr = (vmask[i] >> t) & 1u ? smem + aoff : smem + OFF_ZERO + (aoff & 255);
         fa[i] = *reinterpret_cast<const bf16x8*>(ptr);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int n = 32 * j + lr;
-        fb[j] = *reinterpret_cast<const bf16x8*>(bslot + n * ROWB + 16 * (cg ^ sw(n)));
+        const int n = 64 * wn + 32 * j + lr;
+        fb[j] = *reinterpret_cast<const bf16x8*>(bslot + n * WB + 16 * (gb ^ sw<WB>(n)));
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
+  };
+  if constexpr (NKT <= 9) {
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) ktile(kt);
+  } else {
+    for (int kt = 0; kt < NKT; ++kt) ktile(kt);
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo / ring free for the epilogue
 
-  // ---- epilogue (tile 6's): per 32-row block, re-lay through the wave's LDS rows, 8 channels
+  // ---- epilogue (the generic tiles'): per 32-row block, re-lay through the wave's LDS rows, 8 channels
   // per lane, bias, residual, ReLU, bf16, one 16-B store ----
   float* wt = reinterpret_cast<float*>(smem) + wid * 32 * EPI_LD;
   const int c8 = lane & 7;
   f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
   if (EPI != PIPNET_EPI_NONE && p.bias) {
-    b0 = ld4(p.bias + 8 * c8);
-    b1 = ld4(p.bias + 8 * c8 + 4);
+    b0 = ld4(p.bias + 64 * wn + 8 * c8);
+    b1 = ld4(p.bias + 64 * wn + 8 * c8 + 4);
   }
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -1379,12 +1407,12 @@ __global__ __launch_bounds__(h64::NT, 2) void conv3x3_bf16_n64_kernel(ConvParams
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int row = 8 * it + (lane >> 3);
-      const int m = m0 + 64 * wid + 32 * i + row;
+      const int m = m0 + 64 * wm + 32 * i + row;
       f32x4 x0 = ld4(wt + row * EPI_LD + 8 * c8), x1 = ld4(wt + row * EPI_LD + 8 * c8 + 4);
       x0 += b0;
       x1 += b1;
       if (EPI == PIPNET_EPI_BIAS_RESID_RELU && m < p.M) {
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + 8 * c8);
+        const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + 64 * wn + 8 * c8);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           x0[e] += (float)r[e];
@@ -1404,7 +1432,7 @@ __global__ __launch_bounds__(h64::NT, 2) void conv3x3_bf16_n64_kernel(ConvParams
         o[e] = (bf16)x0[e];
         o[4 + e] = (bf16)x1[e];
       }
-      if (m < p.M) *reinterpret_cast<bf16x8*>(p.C + (int64_t)m * p.ldc + 8 * c8) = o;
+      if (m < p.M) *reinterpret_cast<bf16x8*>(p.C + (int64_t)m * p.ldc + 64 * wn + 8 * c8) = o;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's writes
   }

@@ -233,7 +233,8 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
                    ppp_ok: bool = False, halo64_ok: bool = False) -> int:
     """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
-    11 = 3x3 stride-1 pad-1 Cin = N = 64 convs (W <= 63) on an LDS input halo (tile 6's arithmetic),
+    11 = 3x3 stride-1 pad-1 Cin = N = 64 (W <= 63) / 128 (W <= 31) convs on an LDS input halo (the
+    arithmetic of tiles 6 / 4),
     8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31, N >= 256),
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 / 8 / 9 on
@@ -273,7 +274,7 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     """rocprof name of the bf16 conv instantiation."""
     t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok, halo64_ok) if tile < 0 else tile
     if t == 11:
-        return f"pipnet_bf16::conv3x3_bf16_n64_kernel<{epilogue}>"
+        return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
         return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}>"
     if t == 8:
@@ -298,8 +299,8 @@ def pack_conv_weight_bf16(w_ohwi: Tensor) -> Tensor:
     return out
 
 
-# Tile 11 (3x3 Cin = N = 64 on the LDS input halo) for automatic launches; False = tile 6, bitwise
-# the same outputs (in-process A/B: tools/ab_toggle.py count_pipnet_amd.kernels.CONV3X3_N64_HALO c3)
+# Tile 11 (3x3 Cin = N = 64 / 128 on the LDS input halo) for automatic launches; False = the generic
+# tile (6 / 4 / 0: bitwise the same outputs) (in-process A/B: tools/ab_toggle.py count_pipnet_amd.kernels.CONV3X3_N64_HALO c3)
 CONV3X3_N64_HALO = True
 
 
@@ -330,10 +331,12 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
                and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     ppp_ok = (aload == 0 and pp_ok and cout % 256 == 0
               and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    halo64_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == 64 and w <= 63 and cout == 64
+    halo64_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == cout
+                 and ((cin == 64 and w <= 63) or (cin == 128 and w <= 31))
                  and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     if halo64_ok and tile < 0 and not CONV3X3_N64_HALO:
-        tile = 6                            # the same arithmetic on the generic N = 64 tile
+        halo64_ok = False                   # the same arithmetic on the generic tile
+        tile = 6 if cout == 64 else bf16_conv_tile(m, cout, pp_ok, kv=k)
     _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok,
                                   halo64_ok=halo64_ok),
             2.0 * m * cout * k,

@@ -258,26 +258,29 @@ def test_conv1x1_bf16_dual_matches_single(gpu, m, cin, n1, n2):
     assert torch.equal(y1, r1) and torch.equal(y2, r2)
 
 
-@pytest.mark.parametrize("b,h,w,epi", [(2, 56, 56, _lib.EPI_BIAS_RELU), (3, 17, 13, _lib.EPI_BIAS_RELU),
-                                      (1, 9, 63, _lib.EPI_BIAS), (2, 11, 7, _lib.EPI_BIAS_RESID_RELU),
-                                      (1, 5, 5, _lib.EPI_NONE), (5, 1, 1, _lib.EPI_BIAS_RELU)])
-def test_conv3x3_n64_halo(gpu, b, h, w, epi):
-    """Tile 11 (3x3 s1 p1, Cin = N = 64, LDS input halo) is bitwise equal to tile 6 -- same
-    MFMA shape, same K order, same epilogue -- so choosing it changes no output bit; also
-    against the fp64 conv of the same bf16 values (bf16 output rounding), image-boundary taps,
-    ragged M (rows past the last 256-pixel tile), every epilogue; and batch invariance (image 1
-    alone == image 1 in the batch)."""
-    cin = 64
+@pytest.mark.parametrize("cin,b,h,w,epi", [
+    (64, 2, 56, 56, _lib.EPI_BIAS_RELU), (64, 3, 17, 13, _lib.EPI_BIAS_RELU), (64, 1, 9, 63, _lib.EPI_BIAS),
+    (64, 2, 11, 7, _lib.EPI_BIAS_RESID_RELU), (64, 1, 5, 5, _lib.EPI_NONE), (64, 5, 1, 1, _lib.EPI_BIAS_RELU),
+    (128, 3, 28, 28, _lib.EPI_BIAS_RELU), (128, 2, 13, 31, _lib.EPI_BIAS_RESID_RELU), (128, 1, 7, 3, _lib.EPI_BIAS),
+    (128, 4, 2, 1, _lib.EPI_NONE)])
+def test_conv3x3_n64_halo(gpu, cin, b, h, w, epi):
+    """Tile 11 (3x3 s1 p1, Cin = N = 64 / 128, LDS input halo) is bitwise equal to the generic
+    tile of the layer (6 at N = 64; 4 and 0 at N = 128) -- same MFMA shape, same K order, same
+    epilogue -- so choosing it changes no output bit; also against the fp64 conv of the same
+    bf16 values (bf16 output rounding), image-boundary taps, ragged M (rows past the last tile),
+    every epilogue; and batch invariance (image 1 alone == image 1 in the batch)."""
+    cout = cin
     g = torch.Generator().manual_seed(cin + h * w + b)
     x = torch.randn(b, h, w, cin, generator=g).to(torch.bfloat16)
-    wt = (torch.randn(64, 3, 3, cin, generator=g) * 0.05).to(torch.bfloat16)
-    bias = torch.randn(64, generator=g)
-    r = torch.randn(b, h, w, 64, generator=g).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
+    wt = (torch.randn(cout, 3, 3, cin, generator=g) * 0.05).to(torch.bfloat16)
+    bias = torch.randn(cout, generator=g)
+    r = torch.randn(b, h, w, cout, generator=g).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
     wp = K.pack_conv_weight_bf16(wt.float().to(gpu))
     run = lambda xx, rr, t: K.conv2d_nhwc_bf16(xx.to(gpu), wp, 3, 3, bias.to(gpu), 1, 1, epi,  # noqa: E731
                                                None if rr is None else rr.to(gpu), tile=t)
     out11 = run(x, r, 11)
-    assert torch.equal(out11, run(x, r, 6))
+    for t in ((6,) if cin == 64 else (4, 0)):
+        assert torch.equal(out11, run(x, r, t)), t
     out = out11.double().cpu()
     ref = F.conv2d(x.double().permute(0, 3, 1, 2), wt.double().permute(0, 3, 1, 2), padding=1)
     if epi != _lib.EPI_NONE:
@@ -295,10 +298,11 @@ def test_conv3x3_n64_halo(gpu, b, h, w, epi):
 
 
 def test_conv3x3_n64_halo_rejects(gpu):
-    """Tile 11 forced on a layer outside its scope (Cin != 64, W > 63) is an argument error."""
-    for cin, w in ((32, 8), (64, 64)):
+    """Tile 11 forced on a layer outside its scope (Cin != N, Cin not 64 / 128, W over the halo)
+    is an argument error."""
+    for cin, cout, w in ((32, 64, 8), (64, 64, 64), (128, 128, 32), (64, 128, 8), (256, 256, 8)):
         x = torch.zeros(1, 4, w, cin, dtype=torch.bfloat16, device=gpu)
-        wp = K.pack_conv_weight_bf16(torch.zeros(64, 3, 3, cin, device=gpu))
+        wp = K.pack_conv_weight_bf16(torch.zeros(cout, 3, 3, cin, device=gpu))
         with pytest.raises(RuntimeError):
             K.conv2d_nhwc_bf16(x, wp, 3, 3, None, 1, 1, _lib.EPI_NONE, None, tile=11)
 
