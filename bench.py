@@ -174,20 +174,29 @@ class GemmTimer:
 
 def measured_traffic(dom):
     """HBM bytes per launch of the dominant kernel from the committed PMC measurement
-    (tools/pmc.sh -> tools/pmc_summary.py -> profiles/traffic_latest.json), used only when it
-    was measured on this exact kernel: same kernel name AND same sha256 of the kernel
-    family's sources.  Otherwise (kernel changed since the PMC pass) traffic is null."""
+    (tools/pmc.sh -> tools/pmc_summary.py -> profiles/traffic_latest.json for the headline's
+    GEMM, profiles/traffic_kernels.json for the C3 / C5 kernels), used only when it was
+    measured on this exact kernel: same kernel name AND same sha256 of the kernel family's
+    sources.  Otherwise (kernel changed since the PMC pass) traffic is null."""
     from count_pipnet_amd.build import kernel_source_digest
-    path = os.path.join(REPO, "profiles", "traffic_latest.json")
-    if not os.path.exists(path):
-        return None, "no PMC measurement"
-    with open(path) as f:
-        tr = json.load(f)
-    if tr.get("kernel_key") != dom:
-        return None, f"PMC measurement is of another kernel ({tr.get('kernel_key')})"
+    tr = None
+    for name in ("traffic_latest.json", "traffic_kernels.json"):
+        path = os.path.join(REPO, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            d = json.load(f)
+        if name == "traffic_latest.json" and d.get("kernel_key") == dom:
+            tr, src = d, name
+            break
+        if name == "traffic_kernels.json" and dom in d:
+            tr, src = d[dom], name
+            break
+    if tr is None:
+        return None, "no PMC measurement of this kernel"
     if not tr.get("source_digest") or tr["source_digest"] != kernel_source_digest(dom):
         return None, "PMC measurement predates the current kernel sources (digest mismatch)"
-    return tr.get("hbm_bytes_per_launch"), "profiles/traffic_latest.json (" + tr.get("method", "") + ")"
+    return tr.get("hbm_bytes_per_launch"), f"profiles/{src} (" + tr.get("method", "") + ")"
 
 
 def _cpu_model():
@@ -332,8 +341,10 @@ def main():
         dom = max(agg, key=lambda k: agg[k][2])
         n_l, fl, tt = agg[dom]
         peak = peak_of(dom)
+        traffic, source = measured_traffic(dom)
         return dom, {"bound": "mfma", "kernel": dom, "achieved": fl / tt / 1e12, "peak": peak, "unit": "TFLOP/s",
-                     "frac": fl / tt / 1e12 / peak, "traffic": None, "launches_per_step": n_l / steps,
+                     "frac": fl / tt / 1e12 / peak, "traffic": traffic, "traffic_source": source,
+                     "launches_per_step": n_l / steps,
                      "avg_launch_us": tt / n_l * 1e6, "algorithmic_gflop_per_launch": fl / n_l / 1e9}
 
     def peak_for(split):
@@ -392,7 +403,6 @@ def main():
                      "ms_per_step": gemm_time / a.steps * 1e3, "pass": "roofline pass (one stream)"},
     }
     result.update(info)
-    result["roofline"]["traffic"], result["roofline"]["traffic_source"] = measured_traffic(dom)
     if a.alt_precision != "none" and a.alt_precision != a.precision:
         # the same network and inputs with the other GEMM precision, timed the same way
         from count_pipnet_amd.pipnet import set_hip_dtype

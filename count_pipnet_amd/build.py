@@ -49,6 +49,7 @@ DIGEST_FILE = LIB + ".digest"
 KERNEL_SOURCES = {
     "pipnet_gemm::": ["gemm_f32.hip", "gemm_f32_impl.hpp", "common.hpp"],
     "pipnet_bf16::": ["conv_bf16.hip", "gemm_bf16_impl.hpp", "common.hpp"],
+    "cnblock_mlp_kernel": ["mlp_f32.hip", "common.hpp"],
 }
 
 

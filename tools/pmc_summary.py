@@ -53,6 +53,15 @@ for k, c in sorted(agg.items(), key=lambda kv: -sum(kv[1].get("dur_ns_p1", [0]))
     out[k] = dict(launches=n, avg_us=dur / 1e3, clock_ghz=clk, mfma_busy=mfu, sq_busy=busy,
                   hbm_read_bytes=rd, hbm_write_bytes=wr, hbm_bytes=rd + wr)
 json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)
+# every kernel whose source family is known -> traffic_kernels.json (bench.py's C3 / C5 roofline
+# blocks look their dominant kernel up in profiles/traffic_kernels.json, same digest rule)
+METHOD = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh); "
+          "FETCH_SIZE x2 (gfx950 wide-read undercount), KB -> bytes")
+per = {k: dict(hbm_bytes_per_launch=v["hbm_bytes"], hbm_read_bytes_per_launch=v["hbm_read_bytes"],
+               hbm_write_bytes_per_launch=v["hbm_write_bytes"], avg_us=v["avg_us"], launches=v["launches"],
+               mfma_busy=v["mfma_busy"], source_digest=kernel_source_digest(k), method=METHOD)
+       for k, v in out.items() if kernel_source_digest(k)}
+json.dump(per, open(os.path.join(d, "traffic_kernels.json"), "w"), indent=1)
 # the dominant MFMA kernel (largest total time) -> bench.py roofline.traffic
 gemms = {k: v for k, v in out.items() if "gemm_f32_tn" in k}
 if gemms:
@@ -61,7 +70,6 @@ if gemms:
               hbm_read_bytes_per_launch=gemms[dom]["hbm_read_bytes"],
               hbm_write_bytes_per_launch=gemms[dom]["hbm_write_bytes"], avg_us=gemms[dom]["avg_us"],
               source_digest=kernel_source_digest(dom),
-              method="rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/pmc.sh); "
-                     "FETCH_SIZE x2 (gfx950 wide-read undercount), KB -> bytes")
+              method=METHOD)
     json.dump(tr, open(os.path.join(d, "traffic_latest.json"), "w"), indent=1)
     print("dominant:", json.dumps(tr))
