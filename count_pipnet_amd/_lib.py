@@ -51,6 +51,7 @@ SIGNATURES = {
     "pipnet_maxpool2d_nhwc_bf16": [P, I32, I32, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_nhwc_bf16": [P, I32, I32, I32, I32, I32, P, P],
     "pipnet_nchw_to_s2d_bf16": [P, I32, I32, I32, P, P],
+    "pipnet_stem_pool_bf16": [P, I32, I32, I32, P, P, P, P],
     "pipnet_conv1x1_bf16_dual": [P, I64, I32, P, P, I32, P, I32, P, P],
     "pipnet_softmax_pool_bf16": [P, I32, I32, I32, I32, P, P, P],
     "pipnet_eval_batch_f32": [P, P, P, I32, I32, I32, P, P, F32, P, P, P, P, P, P, P],

@@ -446,6 +446,24 @@ extern "C" int pipnet_nchw_to_s2d_bf16(const float* x, int B, int H, int W, void
   return PIPNET_OK;
 }
 
+// ResNet stem (4x4 stride-1 conv over the s2d image, 16 -> 64, + bias + ReLU) fused with
+// MaxPool2d(3, 2, 1): s2d [B][SH][SW][16] bf16 (pipnet_nchw_to_s2d_bf16), w packed [64][256]
+// (pipnet_pack_conv_weight_bf16 of the regrouped 4x4x16 stem weight), y [B][PH][PW][64] bf16
+// with PH = (SH - 4) / 2 + 1.  Bitwise the unfused conv (tile 6) + pipnet_maxpool2d_nhwc_bf16.
+extern "C" int pipnet_stem_pool_bf16(const void* s2d, int B, int SH, int SW, const void* w, const float* bias,
+                                     void* y, void* stream) {
+  if (B < 0 || SH < 4 || SW < 4 || SW - 3 > spool::MAX_OW || !s2d || !w || !bias || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(s2d) || !aligned16(w) || !aligned16(y)) return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  const int PH = (SH - 3 - 1) / 2 + 1, PW = (SW - 3 - 1) / 2 + 1;
+  const int npr = (PH + spool::PR - 1) / spool::PR;
+  hipLaunchKernelGGL(stem_pool_bf16_kernel, dim3((unsigned)(B * npr)), dim3(spool::NT), 0, (hipStream_t)stream,
+                     reinterpret_cast<const bf16*>(s2d), SH, SW, reinterpret_cast<const bf16*>(w), bias,
+                     reinterpret_cast<bf16*>(y), PH, PW);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
+
 extern "C" int pipnet_maxpool2d_nhwc_bf16(const void* x, int B, int H, int W, int C, int k, int stride, int pad,
                                           void* y, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || (C & 7) || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)

@@ -1438,4 +1438,142 @@ __global__ __launch_bounds__(hsm::NT, 2) void conv3x3_bf16_hsmall_kernel(ConvPar
   }
 }
 
+
+// ======================================================================================
+// ResNet stem fused with its max-pool (bf16 build): the 4x4 stride-1 conv over the 2x2
+// space-to-depth image (Cin 16, N 64, K 256; resnet_features.py:161-163 conv1 + bn1 + relu,
+// see pipnet_nchw_to_s2d_bf16) + bias + ReLU, then MaxPool2d(3, 2, 1) (resnet_features.py:164).
+// Unfused, the stem writes a 112x112x64 bf16 map (103 MB per 64 images) that the pool reads
+// back.  Here one workgroup owns PR = 2 pooled rows of one image: it computes the 2 PR + 1 = 5
+// stem rows they need (1.25x the stem's MFMAs), keeps them in LDS as bf16 and writes only
+// the pooled rows.  The 8 s2d input rows (<= 30 KiB) and all of W (64 x 256, 32 KiB) are
+// staged once by LDS-DMA; 6 waves x 3 blocks of 32 stem pixels x 2 blocks of 32 channels.
+// Arithmetic is tile 6's, bit for bit (MFMA 32x32x16, 32-deep K-tiles of 2 taps, half-wave
+// h = tap 2 kt + h, k-step q = channels 8 q .. +7; bias + ReLU + RNE to bf16), and the pool
+// is maxpool_nhwc_bf16_kernel's (fmaxf from -inf over (ky, kx) in order), so the pooled map
+// is bitwise the unfused one's (tests/test_gpu_bf16.py::test_stem_pool_bf16_matches_unfused).
+// LDS rows: input pixel q's two 16-B chunks at c ^ ((q >> 3) & 1); weight row n's 32 chunks
+// at c ^ (n & 15).  The stem rows re-use the staging area once every wave has finished.
+// Requirements: OW = SW - 3 <= 112, 16-B aligned tensors.
+// ======================================================================================
+namespace spool {
+constexpr int NT = 384, PR = 2, SR = 2 * PR + 1, IR = SR + 3, N = 64, K = 256;
+constexpr int MAX_OW = 112, BLOCKS = 18;              // 18 x 32 >= SR x MAX_OW = 560 stem pixels
+constexpr int IN_BYTES = 30 * 1024, OFF_WT = IN_BYTES, WT_BYTES = N * K * 2;
+constexpr int OUT_BYTES = SR * MAX_OW * N * 2;        // 70 KiB of bf16 stem rows
+constexpr int SMEM = OUT_BYTES > OFF_WT + WT_BYTES ? OUT_BYTES : OFF_WT + WT_BYTES;
+static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
+static_assert(BLOCKS * 32 >= SR * MAX_OW && BLOCKS == 3 * (NT / 64), "3 blocks per wave");
+}  // namespace spool
+
+__global__ __launch_bounds__(spool::NT, 2) void stem_pool_bf16_kernel(const bf16* __restrict__ S, int SH, int SW,
+                                                                      const bf16* __restrict__ Wp,
+                                                                      const float* __restrict__ bias,
+                                                                      bf16* __restrict__ Y, int PH, int PW) {
+  using namespace spool;
+  __shared__ __attribute__((aligned(256))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int npr = (PH + PR - 1) / PR;
+  const int b = blockIdx.x / npr, pr = blockIdx.x - b * npr;
+  const int OH = SH - 3, OW = SW - 3;
+  const int oy0 = 2 * PR * pr - 1;                     // stem row of local row 0
+
+  // ---- LDS-DMA: input rows oy0 .. oy0 + 7 (clamped; rows outside feed only discarded stem rows)
+  auto dma = [&](const bf16* src, int off) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(smem + off), 16, 0, 0);
+  };
+  const int npix = IR * SW, npin = (npix + 31) / 32;
+  for (int pc = wid; pc < npin; pc += NT / 64) {
+    const int q = min(32 * pc + (lane >> 1), npix - 1);
+    const int rr = q / SW, x = q - rr * SW;
+    const int iy = min(max(oy0 + rr, 0), SH - 1);
+    dma(S + (((int64_t)b * SH + iy) * SW + x) * 16 + 8 * ((lane & 1) ^ ((q >> 3) & 1)), pc * 1024);
+  }
+  for (int pc = wid; pc < WT_BYTES / 1024; pc += NT / 64) {
+    const int n = 2 * pc + (lane >> 5), sl = lane & 31;
+    dma(Wp + n * K + 8 * (sl ^ (n & 15)), OFF_WT + pc * 1024);
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- MFMAs: this wave's blocks 3 wid + i, lane row = stem pixel m = 32 blk + (lane & 31)
+  const int lr = lane & 31, lh = lane >> 5;
+  int q0[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int m = 32 * (3 * wid + i) + lr;
+    const int r = m / OW, ox = m - r * OW;
+    q0[i] = m < SR * OW ? r * SW + ox : 0;             // padding rows read row 0, then are dropped
+  }
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[i][j][v] = 0.f;
+#pragma unroll 2
+  for (int kt = 0; kt < K / 32; ++kt) {
+    const int tap = 2 * kt + lh, a = tap >> 2, a2 = tap & 3;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      bf16x8 fa[3], fb[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int qp = q0[i] + a * SW + a2;
+        fa[i] = *reinterpret_cast<const bf16x8*>(smem + qp * 32 + 16 * (qq ^ ((qp >> 3) & 1)));
+      }
+      const int c = 4 * kt + 2 * lh + qq;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 32 * j + lr;
+        fb[j] = *reinterpret_cast<const bf16x8*>(smem + OFF_WT + n * 512 + 16 * (c ^ (n & 15)));
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // staging area free
+
+  // ---- stem rows to LDS as bf16: relu(acc + b), rounded as tile 6's epilogue rounds ----
+  bf16* out = reinterpret_cast<bf16*>(smem);
+  const float bj[2] = {bias[lr], bias[32 + lr]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int m = 32 * (3 * wid + i) + (v & 3) + 8 * (v >> 2) + 4 * lh;
+        if (m < SR * OW) out[m * N + 32 * j + lr] = (bf16)fmaxf(acc[i][j][v] + bj[j], 0.f);
+      }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- MaxPool2d(3, 2, 1) over the stem rows, 8 channels per item ----
+  for (int it = tid; it < PR * PW * 8; it += NT) {
+    const int c8 = it & 7, px = (it >> 3) % PW, py = PR * pr + (it >> 3) / PW;
+    if (py >= PH) continue;
+    float mx[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int oy = 2 * py - 1 + ky;
+      if (oy < 0 || oy >= OH) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ox = 2 * px - 1 + kx;
+        if (ox < 0 || ox >= OW) continue;
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(out + ((oy - oy0) * OW + ox) * N + 8 * c8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)mx[e];
+    *reinterpret_cast<bf16x8*>(Y + (((int64_t)b * PH + py) * PW + px) * N + 8 * c8) = o;
+  }
+}
+
 }  // namespace pipnet_bf16

@@ -346,6 +346,24 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     return y
 
 
+def stem_pool_bf16(s2d: Tensor, w_packed: Tensor, bias: Tensor) -> Tensor:
+    """ResNet stem over the space-to-depth image (4x4 stride 1, 16 -> 64, + bias + ReLU) fused
+    with MaxPool2d(3, 2, 1) (pipnet_stem_pool_bf16): bitwise conv2d_nhwc_bf16 + maxpool2d_nhwc_bf16."""
+    _chk_bf(s2d, "stem s2d input")
+    _chk_bf(w_packed, "stem weight")
+    _chk(bias, "stem bias")
+    b, sh, sw, c = s2d.shape
+    if c != 16 or tuple(w_packed.shape) != (64, 256):
+        raise RuntimeError(f"stem_pool_bf16: expects a 16-channel s2d image and a [64, 256] weight, got "
+                           f"{tuple(s2d.shape)} / {tuple(w_packed.shape)}")
+    ph, pw = (sh - 4) // 2 + 1, (sw - 4) // 2 + 1
+    y = torch.empty((b, ph, pw, 64), device=s2d.device, dtype=torch.bfloat16)
+    _launch("pipnet_bf16::stem_pool_bf16_kernel", 2.0 * b * (sh - 3) * (sw - 3) * 64 * 256,
+            lambda: _lib.call("pipnet_stem_pool_bf16", s2d.data_ptr(), b, sh, sw, w_packed.data_ptr(),
+                              bias.data_ptr(), y.data_ptr(), _stream(s2d)))
+    return y
+
+
 def maxpool2d_nhwc_bf16(x: Tensor, k: int, stride: int, pad: int) -> Tensor:
     _chk_bf(x, "maxpool input")
     b, h, w, c = x.shape

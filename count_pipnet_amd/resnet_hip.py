@@ -81,6 +81,9 @@ def _conv_bn(cache, key, conv, bn, x, epilogue, r=None, cpad=None):
 
 
 DUAL_1X1 = True      # tools / A-B runs may switch the dual downsample + conv1 launch off
+# bf16 stem fused with its max-pool (pipnet_stem_pool_bf16); False = conv + pool launches, bitwise
+# the same map (A/B: tools/ab_toggle.py count_pipnet_amd.resnet_hip.STEM_POOL c3)
+STEM_POOL = True
 
 
 def _dual_ok(blk, h) -> bool:
@@ -145,11 +148,15 @@ def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
                 and c1.dilation == (1, 1):
             # space-to-depth stem: a 4x4 stride-1 conv with K = 256 instead of 7x7x8 -> 448
             w, b = _stem_s2d(cache, c1, model.bn1)
-            h = K.conv2d_nhwc_bf16(K.nchw_to_s2d_bf16(x), w, 4, 4, b, 1, 0, _lib.EPI_BIAS_RELU)
+            s2d = K.nchw_to_s2d_bf16(x)
+            if STEM_POOL and c1.out_channels == 64 and s2d.shape[2] - 3 <= 112:
+                h = K.stem_pool_bf16(s2d, w, b)           # conv + bias + ReLU + max-pool, one launch
+            else:
+                h = K.maxpool2d_nhwc_bf16(K.conv2d_nhwc_bf16(s2d, w, 4, 4, b, 1, 0, _lib.EPI_BIAS_RELU), 3, 2, 1)
         else:
             h = K.nchw_to_nhwc_bf16(x, 8)
             h = _conv_bn(cache, "stem", c1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=8)
-        h = K.maxpool2d_nhwc_bf16(h, 3, 2, 1)
+            h = K.maxpool2d_nhwc_bf16(h, 3, 2, 1)
     else:
         h = K.nchw_to_nhwc(x, 4)
         h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=4)

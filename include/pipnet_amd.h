@@ -219,6 +219,14 @@ int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_pa
  * y[b][i][j][(2 bi + bj) * 4 + c] = x[b][c][2(i-2)+bi][2(j-2)+bj] (zero outside the image and for
  * c = 3).  The matching weights are W'[o][a][a'][(2 bi + bj) * 4 + c] = w[o][c][2a+bi-1][2a'+bj-1]. */
 int pipnet_nchw_to_s2d_bf16(const float* x, int B, int H, int W, void* y, void* stream);
+/* ResNet stem (4x4 stride-1 conv over the s2d image, 16 -> 64 channels, + bias + ReLU) fused
+ * with MaxPool2d(3, 2, 1) -- replaces the conv1 / bn1 / relu / maxpool sequence of
+ * resnet_features.py:161-164 in the bf16 build.  s2d: [B][SH][SW][16] bf16 from
+ * pipnet_nchw_to_s2d_bf16; w: packed [64][256] bf16 (the regrouped 4x4x16 stem weight, BN
+ * folded); bias: [64] fp32; y: [B][PH][PW][64] bf16, PH = (SH - 4) / 2 + 1.  SW - 3 <= 112.
+ * Bitwise equal to pipnet_conv2d_nhwc_bf16 (4x4, EPI_BIAS_RELU) + pipnet_maxpool2d_nhwc_bf16. */
+int pipnet_stem_pool_bf16(const void* s2d, int B, int SH, int SW, const void* w, const float* bias, void* y,
+                          void* stream);
 
 /* pipnet_softmax_pool_f32 reading bf16 logits (fp32 softmax, fp32 proto / pooled out). */
 int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,

@@ -307,6 +307,24 @@ def test_conv3x3_n64_halo_rejects(gpu):
             K.conv2d_nhwc_bf16(x, wp, 3, 3, None, 1, 1, _lib.EPI_NONE, None, tile=11)
 
 
+@pytest.mark.parametrize("b,h,w", [(3, 224, 224), (2, 37, 53), (1, 9, 9), (2, 224, 100), (1, 5, 224)])
+def test_stem_pool_bf16_matches_unfused(gpu, b, h, w):
+    """The fused stem + max-pool (pipnet_stem_pool_bf16) is bitwise the unfused pair: the 4x4
+    s2d conv on its automatic tile (6) with bias + ReLU, then pipnet_maxpool2d_nhwc_bf16 --
+    odd sizes put pooled rows past the image, partial last row pairs and 1-row maps in play."""
+    g = torch.Generator().manual_seed(b * 1000 + h * 7 + w)
+    x = torch.randn(b, 3, h, w, generator=g).to(gpu)
+    w7 = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    wp = K.pack_conv_weight_bf16(K.stem_weight_s2d(w7.permute(0, 2, 3, 1).contiguous()).to(gpu))
+    bias = (torch.randn(64, generator=g) * 0.1).to(gpu)
+    s2d = K.nchw_to_s2d_bf16(x)
+    fused = K.stem_pool_bf16(s2d, wp, bias)
+    ref = K.maxpool2d_nhwc_bf16(K.conv2d_nhwc_bf16(s2d, wp, 4, 4, bias, 1, 0, _lib.EPI_BIAS_RELU), 3, 2, 1)
+    torch.cuda.synchronize()
+    assert fused.shape == ref.shape
+    assert torch.equal(fused, ref)
+
+
 def _c3_bf16(gpu, num_features=0):
     from golden_util import golden_args, golden_inputs, golden_state_dict, load_golden
     from model_util import build_model

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("config")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--stream-split", type=int, default=0, help="0 = the model's default")
     a = ap.parse_args()
     modname, attr = a.flag.rsplit(".", 1)
     mod = importlib.import_module(modname)
@@ -30,6 +31,9 @@ def main():
     cfg = bc.CONFIGS[a.config]
     net = bc.make(cfg, dev)
     xs = synth_images(cfg["batch"], cfg["size"], seed=1).to(dev)
+    if a.stream_split:
+        from count_pipnet_amd.pipnet import set_stream_split
+        set_stream_split(net, a.stream_split)
     res = {False: [], True: []}
     outs = {}
     with torch.no_grad():
@@ -51,7 +55,8 @@ def main():
     same = all(torch.equal(x, y) for x, y in zip(outs[False], outs[True]))
     for val in (False, True):
         ms = sorted(res[val])
-        print(json.dumps({"flag": a.flag, "value": val, "config": a.config, "ms_median": ms[len(ms) // 2],
+        print(json.dumps({"flag": a.flag, "value": val, "config": a.config, "stream_split": a.stream_split or "default",
+                          "ms_median": ms[len(ms) // 2],
                           "ms_min": ms[0], "img_s_median": cfg["batch"] / ms[len(ms) // 2] * 1e3}))
     print(json.dumps({"outputs_bitwise_equal": same}))
 
