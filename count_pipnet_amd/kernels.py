@@ -82,6 +82,7 @@ def gemm_persist(mode: int = -1) -> bool:
 
 
 SPLITK_WG_PER_CU = int(os.environ.get("PIPNET_SPLITK_WG_PER_CU", "2"))   # env: A/B runs (tools)
+SPLITK_MIN_K = int(os.environ.get("PIPNET_SPLITK_MIN_K", "256"))          # env: A/B runs (tools)
 
 
 def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
@@ -94,7 +95,7 @@ def splitk_factor(m: int, n: int, k: int, cus: int = 256) -> int:
     tiles = -(-m // 64) * -(-n // 128)
     if tiles >= cus:
         return 1
-    return max(1, min(-(-SPLITK_WG_PER_CU * cus // tiles), k // 256, 64))
+    return max(1, min(-(-SPLITK_WG_PER_CU * cus // tiles), k // SPLITK_MIN_K, 64))
 
 
 def _ptr(t: Optional[Tensor]) -> Optional[int]:
