@@ -926,7 +926,10 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       setup(id, m0, n0);
       prologue_dma();
     }
-    // ---- epilogue: 8 pieces of 16 rows per wave through the wave's 4 KiB region ----
+    // ---- epilogue: 8 pieces of 16 rows per wave through the wave's 4 KiB region.  Identity
+    // loads and output stores are non-temporal: C3 21.6k -> 22.1k img/s median over five
+    // interleaved runs (profiles/r03/ppp_nt_epilogue_ab.log) -- fewer caches lines for this
+    // stream of read-once / written-once tiles; bits unchanged ----
     float* wt = reinterpret_cast<float*>(smem + ppp::OFF_EPI) + wid * 16 * 64;
     const int c8 = lane & 7;
     const int n = cn0 + wc * 64 + 8 * c8;
@@ -945,7 +948,8 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int m = min(cm0 + wr * 128 + q * 8 + (lane >> 3), p.M - 1);
-        rr[q] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
+        rr[q] = __builtin_bit_cast(bf16x8v, __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x4*>(p.R + (int64_t)m * p.ldr + n)));   // read once
       }
     }
     const int fq = lane >> 4;
@@ -988,7 +992,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
           o[4 + e] = (bf16)x1[e];
         }
         const int m = min(cm0 + wr * 128 + r * 16 + row, p.M - 1);
-        *reinterpret_cast<bf16x8v*>(cout + (int64_t)m * ldo + no) = o;
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(cout + (int64_t)m * ldo + no));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
