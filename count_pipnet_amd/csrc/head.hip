@@ -67,7 +67,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
       const int c = lane + 64 * j;
       if (c < P) {
         const float yv = v[j] * inv;
-        proto[base + c] = yv;
+        __builtin_nontemporal_store(yv, proto + base + c);   // written once, never re-read here
         racc[j] = MODE == 0 ? fmaxf(racc[j], yv) : racc[j] + yv;
       }
     }
@@ -155,8 +155,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
         f32x4 y0, y1;
 #pragma unroll
         for (int e = 0; e < 4; ++e) y0[e] = v[j][e] * inv, y1[e] = v[j][4 + e] * inv;
-        st4(proto + base + c, y0);
-        st4(proto + base + c + 4, y1);
+        __builtin_nontemporal_store(y0, reinterpret_cast<f32x4*>(proto + base + c));   // write-once map
+        __builtin_nontemporal_store(y1, reinterpret_cast<f32x4*>(proto + base + c + 4));
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           racc[j][e] = MODE == 0 ? fmaxf(racc[j][e], y0[e]) : racc[j][e] + y0[e];
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
             o[e] = z[j][e] * inv;
             racc[j][e] += o[e];
           }
-          st4(proto + base + c, o);
+          __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(proto + base + c));
         }
       }
       continue;
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (c + e == mi) ? hard : 0.f;
-        st4(proto + base + c, o);
+        __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(proto + base + c));
       }
     }
     if (lane == 0) atomicAdd(hist + (int64_t)b * P + mi, 1);
