@@ -127,7 +127,8 @@ def test_layernorm(gpu, c):
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("p,hw,mode", [(768, 676, 0), (2048, 784, 0), (16, 64, 1), (200, 33, 0), (2048, 256, 1)])
+@pytest.mark.parametrize("p,hw,mode", [(768, 676, 0), (2048, 784, 0), (16, 64, 1), (200, 33, 0), (2048, 256, 1),
+                                        (1000, 50, 1), (1500, 20, 0), (30, 49, 0)])   # P % 4 != 0: lane-strided kernel
 def test_softmax_pool(gpu, p, hw, mode):
     g = torch.Generator().manual_seed(p + hw)
     x = _rand(3, hw, p, gen=g, scale=4.0)
