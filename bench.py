@@ -13,10 +13,12 @@ With ``--gpus N > 1`` and no torchrun environment, bench.py launches its own N r
 ``torch.distributed.run`` child, started before anything touches the GPU) and exits with
 its status; under torchrun, ``WORLD_SIZE`` must equal N.
 
-The same run also times the other GPU configs of BASELINE.json on each rank's shard
-(``extra``): C3 (PIP-Net ResNet-50, 128 images of 224x224, bf16) and C5 (CountPIPNet
-bilinear, 2048 prototypes, 64 images of 128x128 per GPU; BASELINE configs[4] shards 256
-over 4 GPUs), each with its own dominant-kernel roofline.  ``value`` / ``config`` stay C2.
+The same run also times the other GPU configs of BASELINE.json (``extra``), each with its own
+dominant-kernel roofline; ``value`` / ``config`` stay C2.  C3 (PIP-Net ResNet-50, 128 images
+of 224x224, bf16) is a 1-GPU config: at N > 1 every rank runs its own configs[2] batch.  C5
+(CountPIPNet bilinear, 2048 prototypes, 128x128) is configs[4] = 256 images over 4 GPUs: at
+N = 4k it runs as k independent 4-rank groups of exactly that layout, below 4 GPUs as N
+64-image shards of it.  Each ``extra.*.workload`` states which (``extra_layout``).
 
 Prints one JSON line on rank 0 (fields described in DESIGN.md section "Measurement").
 """
@@ -60,8 +62,9 @@ def parse_args(argv=None):
     ap.add_argument("--alt-precision", choices=["none", "fp32", "bf16x3"], default="bf16x3",
                     help="also time this precision on the same network (reported under alt_precision)")
     ap.add_argument("--stream-split", type=int, default=None,
-                    help="override the model's default stream split for the throughput pass (profiling runs use 1 "
-                         "so every launch of a kernel is a full-batch launch, as in the roofline pass)")
+                    help="override the models' default stream split for the throughput pass, C3 / C5 included "
+                         "(profiling runs use 1 so every launch of a kernel is a full-batch launch, as in the "
+                         "roofline pass)")
     ap.add_argument("--dist-backend", default=None,
                     help="rehearsal only: torch.distributed backend (default nccl = RCCL on GPUs)")
     ap.add_argument("--device-index", type=int, default=None,
@@ -117,8 +120,8 @@ EXTRA = {
     "c3": dict(baseline="configs[2]", model="pipnet", batch=128, size=224, classes=200, gflop=38.16,
                gflop_executed=38.16 + 2 * 112 * 112 * 64 * (1.25 * 256 - 147) / 1e9,
                dtype="bf16", peak=PEAK_BF16_TFLOPS,
-               workload="PIP-Net ResNet-50 forward(inference=True), 224x224, 200 classes, bf16 activations / "
-                        "weights with fp32 accumulation, 128 images per GPU",
+               workload_base="PIP-Net ResNet-50 forward(inference=True), 224x224, 200 classes, bf16 activations / "
+                             "weights with fp32 accumulation, 128 images per GPU",
                args=dict(net="resnet50", num_features=0, bias=False, hip_dtype="bf16")),
     # C5: 1.374 GFLOP/img is the reference algorithm's work; the HIP path folds the bilinear
     # intermediate's embedding into W / V (count_pipnet.py _bilinear_folded: 2*(P*D + 2*D^2) ->
@@ -126,12 +129,39 @@ EXTRA = {
     "c5": dict(baseline="configs[4]", model="count", batch=64, size=128, classes=9, gflop=1.374,
                gflop_executed=1.374 - 2 * (2048 * 6144 + 2 * 6144 * 6144 - 2 * 2048 * 6144) / 1e9,
                dtype="f32", peak=PEAK_F32_TFLOPS,
-               workload="CountPIPNet bilinear forward(inference=True), 2048 prototypes, hard Gumbel head "
-                        "(Philox noise), 128x128, 9 classes, 64 images per GPU (configs[4]: 256 over 4 GPUs)",
+               workload_base="CountPIPNet bilinear forward(inference=True), 2048 prototypes, hard Gumbel head "
+                             "(Philox noise), 128x128, 9 classes, 64 images per GPU",
                args=dict(net="convnext_tiny_26", use_mid_layers=True, num_stages=3, num_features=2048,
                          activation="gumbel_softmax", intermediate_layer="bilinear", max_count=3, use_ste=True,
                          bias=False)),
 }
+
+
+def extra_layout(name, world, rank):
+    """How BASELINE config ``name`` runs on ``world`` ranks, and the label that says so exactly.
+    Returns (group ranks or None for the whole world, ranks per group, workload label).
+    * c3 = configs[2], a 1-GPU config: every rank runs its own 128-image configs[2] batch (a
+      per-rank replica), the N shards joined by the all-gather of logits / pooled.
+    * c5 = configs[4], 256 images over 4 GPUs (64 per GPU): for N a multiple of 4 the world is cut
+      into N / 4 independent 4-rank groups, each running configs[4] exactly (all-gather inside its
+      group); for N < 4 (or not a multiple of 4) the N ranks run 64-image shards of its layout."""
+    cfg = EXTRA[name]
+    if name == "c5":
+        if world >= 4 and world % 4 == 0:
+            g = rank // 4
+            label = (f"{cfg['workload_base']}, BASELINE configs[4] exactly: 256 images over 4 GPUs (64 per GPU), "
+                     f"run as {world // 4} independent 4-rank group(s) with the all-gather inside each group "
+                     f"({world * cfg['batch']} images per step in all)")
+            return (list(range(4 * g, 4 * g + 4)) if world > 4 else None), 4, label
+        label = (f"{cfg['workload_base']}, {world} rank(s) x 64-image shards of BASELINE configs[4]'s layout "
+                 f"(configs[4] itself is 256 images over 4 GPUs)"
+                 + (", all-gather over the ranks" if world > 1 else ""))
+        return None, world, label
+    if world == 1:
+        return None, 1, f"{cfg['workload_base']}, BASELINE configs[2] (1 GPU)"
+    return None, world, (f"{cfg['workload_base']}; BASELINE configs[2] is a 1-GPU config: each of the {world} ranks "
+                         f"runs its own configs[2] batch (per-rank replica, {world * cfg['batch']} images per step), "
+                         f"all-gather of logits / pooled over the {world} ranks")
 
 
 def make_extra(cfg, dev):
@@ -308,7 +338,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    def timed(model, inp, batch, steps, warmup, instrument=False):
+    def timed(model, inp, batch, steps, warmup, instrument=False, gw=None):
         """W warm-up steps, then K steps bracketed by barrier + synchronize, max over ranks.
         ``instrument``: every MFMA GEMM / conv launch in the timed region is bracketed by HIP
         events on the stream it is launched on (torch's current stream) for the
@@ -316,7 +346,7 @@ def main():
         ``value``."""
         def step():
             with torch.no_grad():
-                model(inp, inference=True, global_batch=False, sizes=[batch] * world)
+                model(inp, inference=True, global_batch=False, sizes=[batch] * (gw or world))
         for _ in range(warmup):
             step()
         timer = GemmTimer()
@@ -358,14 +388,16 @@ def main():
 
     from count_pipnet_amd.pipnet import set_stream_split, stream_split
 
-    def measure(model, inner, inp, batch, steps, peak_of):
+    def measure(model, inner, inp, batch, steps, peak_of, gw=None):
         """Throughput with the model's default stream split (clean pass), then the roofline
         pass: one stream (per-kernel events must not overlap another stream's kernels),
-        instrumented.  Returns (elapsed, roofline dict, agg, extra fields)."""
+        instrumented.  ``gw``: ranks in the model's process group (default: the world); the
+        barriers and the max-over-ranks time always span the whole world.  Returns (elapsed,
+        roofline dict, agg, extra fields)."""
         nsplit = stream_split(inner, inp)
-        el, _ = timed(model, inp, batch, steps, a.warmup)
+        el, _ = timed(model, inp, batch, steps, a.warmup, gw=gw)
         set_stream_split(inner, 1)
-        el1, agg = timed(model, inp, batch, steps, max(1, a.warmup // 2), instrument=True)
+        el1, agg = timed(model, inp, batch, steps, max(1, a.warmup // 2), instrument=True, gw=gw)
         set_stream_split(inner, nsplit)
         _, roof = roofline(agg, steps, peak_of)
         info = {"stream_split": nsplit, "roofline_pass": {"streams": 1, "instrumented": True,
@@ -429,13 +461,23 @@ def main():
         extra = {}
         for name, cfg in EXTRA.items():
             enet = make_extra(cfg, dev)
-            ewrap = ShardedInference(enet)
+            granks, gw, label = extra_layout(name, world, rank)
+            group = None
+            if world > 1 and granks is not None:
+                # every rank creates every group, in the same order (torch.distributed contract)
+                groups = [dist.new_group(list(range(g0, g0 + gw))) for g0 in range(0, world, gw)]
+                group = groups[rank // gw]
+            if a.stream_split is not None:
+                set_stream_split(enet, a.stream_split)
+            ewrap = ShardedInference(enet, process_group=group)
             exs = synth_images(cfg["batch"], cfg["size"], seed=200 + rank).to(dev)
             esteps = max(a.steps, 10)
-            el, eroof, _, einfo = measure(ewrap, enet, exs, cfg["batch"], esteps, lambda dom, p=cfg["peak"]: p)
+            el, eroof, _, einfo = measure(ewrap, enet, exs, cfg["batch"], esteps, lambda dom, p=cfg["peak"]: p,
+                                          gw=gw)
             gx = cfg.get("gflop_executed", cfg["gflop"])
             gm = min(gx, cfg["gflop"])   # model TF/s: the smaller of the reference's and the executed FLOPs
-            rec = {"baseline": cfg["baseline"], "workload": cfg["workload"], "dtype": cfg["dtype"],
+            rec = {"baseline": cfg["baseline"], "workload": label, "dtype": cfg["dtype"],
+                   "ranks_per_group": gw, "groups": world // gw,
                    "per_gpu_batch": cfg["batch"], "global_batch": cfg["batch"] * world, "image_size": cfg["size"],
                    "value": cfg["batch"] * world * esteps / el, "unit": "images/sec",
                    "ms_per_step": el / esteps * 1e3, "steps": esteps,

@@ -6,3 +6,5 @@ non-negative linear head), executed by hand-written HIP kernels for gfx950 behin
 C-ABI declared in ``include/pipnet_amd.h``.
 """
 __version__ = "0.1.0"
+
+from .backend import invalidate_weight_caches, torch_backend  # noqa: E402,F401

@@ -39,3 +39,27 @@ def torch_backend():
 
 def use_hip(module: torch.nn.Module) -> bool:
     return (not module.training) and (not torch.is_grad_enabled()) and (not _forced_torch())
+
+
+# Attributes under which modules keep device-layout copies of their parameters (depthwise taps,
+# BN-folded convs, bf16 / split-plane weights, the folded bilinear intermediate).
+_CACHE_ATTRS = ("_hip_pack", "_hip_fold_cache")
+
+
+def invalidate_weight_caches(net: torch.nn.Module) -> int:
+    """Drop every repacked / folded weight copy under ``net``; the next HIP forward rebuilds them.
+
+    The caches are keyed on each parameter's storage pointer and in-place version counter, which
+    every torch in-place op (``optimizer.step()``, ``load_state_dict``, ``param.copy_``) bumps.
+    A write through ``param.data`` (``p.data.copy_(...)``, ``p.data[...] = ...``) goes through a
+    tensor with its OWN version counter, so it is invisible to that stamp: call this after such a
+    write (or write through ``torch.no_grad()`` + ``param.copy_`` instead).  Returns the number
+    of cache dicts cleared.  Captured graphs (``graph.GraphedForward``) must be re-captured."""
+    n = 0
+    for mod in net.modules():
+        for attr in _CACHE_ATTRS:
+            c = mod.__dict__.get(attr)
+            if isinstance(c, dict):
+                c.clear()
+                n += 1
+    return n

@@ -207,7 +207,10 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
     once to fp32) turn the inference intermediate into two M = batch GEMMs with K = P that
     stream 2 D P instead of D P + 2 D^2 weight floats (C5: 101 MB instead of 352 MB, 3.5x fewer
     FLOPs) -- the same kind of inference-time fold as the BatchNorm fold of the ResNet path.
-    Rebuilt whenever any of the three weights changes (storage pointer / in-place version)."""
+    The products run on the in-tree fp64 MFMA kernel (``K.matmul_f64acc``), never a vendor GEMM.
+    Rebuilt whenever any of the three weights changes (storage pointer / in-place version); a
+    write through ``param.data`` bypasses the version counter -- call
+    ``count_pipnet_amd.invalidate_weight_caches(net)`` after one (backend.py)."""
     ts = (layer.embed.weight, layer.W.weight, layer.V.weight)
     stamp = tuple((t.data_ptr(), t._version, tuple(t.shape)) for t in ts)
     cache = layer.__dict__.setdefault("_hip_fold_cache", {})   # plain attribute, not a buffer
@@ -215,9 +218,9 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
     ent = cache.get(key)
     if ent is None or ent[0] != stamp:
         with torch.no_grad():
-            e = layer.embed.weight.detach().double()
-            wf = (layer.W.weight.detach().double() @ e).float().contiguous()
-            vf = (layer.V.weight.detach().double() @ e).float().contiguous()
+            e = layer.embed.weight.detach().contiguous()
+            wf = K.matmul_f64acc(layer.W.weight.detach().contiguous(), e)
+            vf = K.matmul_f64acc(layer.V.weight.detach().contiguous(), e)
         ent = (stamp, (wf, vf))
         cache[key] = ent
     return ent[1]

@@ -13,11 +13,13 @@ gathers all three outputs back to GPU 0.  Here:
   * ``proto_features`` is gathered to rank 0 when the caller uses DataParallel's call
     pattern (the full batch on every rank): DataParallel gathers all three outputs to
     ``device_ids[0]`` and callers index ``proto_features[i]`` across the batch
-    (util/vis_pipnet.py:25).  Other ranks keep their own shard's map, so the map (133 MB per
-    64 ConvNeXt images) crosses xGMI once per shard, not once per rank pair.
-    ``gather_proto=True`` all-gathers it to every rank, ``False`` never gathers; callers that
-    pass their own shard (``global_batch=False``, e.g. bench.py) get their shard's map
-    unless they ask.
+    (util/vis_pipnet.py:25).  The other ranks get ``None`` for it -- the full-batch map is not
+    on their device, and handing them their own shard beside full-batch pooled / logits would
+    make ``proto_features[i]`` silently pick the wrong image -- so the map (133 MB per 64
+    ConvNeXt images) crosses xGMI once per shard, not once per rank pair.
+    ``gather_proto=True`` all-gathers it to every rank, ``False`` never gathers (each rank keeps
+    its shard's map); callers that pass their own shard (``global_batch=False``, e.g.
+    bench.py) get their shard's map unless they ask.
 
 ``ShardedInference`` keeps DataParallel's ``.module`` attribute, so callers written for
 the reference (``net.module._classification``, ``net.module._num_classes`` in
@@ -107,8 +109,9 @@ class ShardedInference(nn.Module):
         rank's own shard (pass ``sizes`` -- every rank's shard size -- to skip the size
         exchange and its host sync).  Returns (proto_features, pooled [B, P], out [B, K]) in global
         batch order.  proto_features covers the whole batch on every rank when ``gather_proto``
-        is True; on rank 0 only when it is None (the default) and ``global_batch`` is True --
-        DataParallel's output placement --; and is this rank's shard otherwise."""
+        is True; when it is None (the default) and ``global_batch`` is True -- DataParallel's
+        output placement -- it covers the whole batch on rank 0 and is ``None`` on every other
+        rank; otherwise it is this rank's shard."""
         world, rank = self.world, self.rank
         if global_batch:
             sizes = shard_sizes(xs.shape[0], world)
@@ -133,6 +136,8 @@ class ShardedInference(nn.Module):
         if world > 1:
             if self.gather_proto is None and global_batch:
                 proto = gather_proto_features(proto, sizes, self.process_group, to_root=True)
+                if rank != 0:
+                    proto = None          # not this rank's to index (see the module docstring)
             elif self.gather_proto:
                 proto = gather_proto_features(proto, sizes, self.process_group)
         return proto, pooled, out

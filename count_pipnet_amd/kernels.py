@@ -148,6 +148,20 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     return out
 
 
+def matmul_f64acc(a: Tensor, b: Tensor) -> Tensor:
+    """[M,K] @ [K,N] (row-major fp32) with fp64 products and sums, rounded once to fp32
+    (include/pipnet_amd.h pipnet_matmul_f64acc_f32): the inference-time weight folds."""
+    _chk(a, "fold operand A")
+    _chk(b, "fold operand B")
+    if a.dim() != 2 or b.dim() != 2 or a.shape[1] != b.shape[0]:
+        raise RuntimeError(f"matmul_f64acc: shapes {tuple(a.shape)} x {tuple(b.shape)}")
+    m, k = a.shape
+    n = b.shape[1]
+    out = torch.empty((m, n), device=a.device, dtype=torch.float32)
+    _lib.call("pipnet_matmul_f64acc_f32", a.data_ptr(), k, b.data_ptr(), n, out.data_ptr(), n, m, n, k, _stream(a))
+    return out
+
+
 def linear_rowscale(a: Tensor, w: Tensor, bias: Optional[Tensor], scale: Tensor, r: Tensor, row_scale: Tensor,
                     rows_per_scale: int) -> Tensor:
     """In place on ``r`` ([M,N]): r = r + row_scale[m // rows_per_scale] * (scale * (a w^T + bias))

@@ -468,6 +468,15 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
                               float w_align, float w_tanh, float tanh_coeff, float inv_tau, float* dcnt_ws,
                               float* d_logits, void* stream);
 
+/* fp64-accumulated product for inference-time weight folds (csrc/fold_f64.hip):
+ *   C[M,N] (ldc) = RNE_f32( sum_k double(A[m,k]) * double(B[k,n]) ), A [M,K] (lda) and B [K,N]
+ *   (ldb) row-major fp32, products and sums in fp64 on v_mfma_f64_16x16x4_f64, any sizes.
+ * Replaces the float64 torch matmul of the BilinearIntermediate fold (the embedding folded into
+ * W and V: W(embed(x)) * V(embed(x)) = (W E) x * (V E) x, count_pipnet_utils.py:378-385) --
+ * run once per weight version, off the steady-state forward. */
+int pipnet_matmul_f64acc_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                             int M, int N, int K, void* stream);
+
 /* ---- ResNet training step (csrc/bn_ops.hip): BatchNorm2d in train mode ------------------
  * Replaces the autograd of nn.BatchNorm2d(C) under net.train() in the ResNet Bottleneck /
  * stem (features/resnet_features.py:77-119, 137-140; pipnet/train.py:14), NHWC rows

@@ -79,3 +79,29 @@ def test_bench_self_launches_two_ranks(gpu):
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 128 and res["config"]["parallelism"] == "dp2"
     assert res["config"]["exchange"] == "gloo all_gather(logits, pooled)"
     assert res["config"]["num_classes"] == 200 and res["value"] > 0
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_extra_labels_state_what_runs(world):
+    """every ``extra.*.workload`` names exactly what ran at N ranks.  C3 is a
+    1-GPU config (a per-rank replica beyond N = 1); C5 is configs[4] (256 over 4 GPUs): exact
+    4-rank groups at N = 4k (two of them at N = 8), 64-image shards of its layout below 4."""
+    import bench
+    for rank in range(world):
+        granks, gw, label = bench.extra_layout("c3", world, rank)
+        assert granks is None and gw == world
+        if world == 1:
+            assert "configs[2] (1 GPU)" in label
+        else:
+            assert "per-rank replica" in label and f"{world * 128} images per step" in label
+        granks, gw, label = bench.extra_layout("c5", world, rank)
+        if world % 4 == 0:
+            assert gw == 4 and "configs[4] exactly" in label and f"{world // 4} independent 4-rank group" in label
+            assert f"{world * 64} images per step" in label
+            if world == 8:
+                assert granks == list(range(4 * (rank // 4), 4 * (rank // 4) + 4)) and rank in granks
+            else:
+                assert granks is None
+        else:
+            assert gw == world and granks is None and "shards of BASELINE configs[4]'s layout" in label
+            assert "256 images over 4 GPUs" in label and "exactly" not in label

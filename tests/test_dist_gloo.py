@@ -47,6 +47,7 @@ def _worker(rank, world, port, batch, q):
                                        sizes=shard_sizes(batch, world))
             # gather_proto=True: the whole map on every rank
             proto4, _, _ = ShardedInference(net, gather_proto=True)(xs, inference=True)
+            proto5, _, _ = ShardedInference(net, gather_proto=False)(xs, inference=True)
             try:
                 wrapped(xs[start:start + own], inference=True, global_batch=False, sizes=[own + 1] * world)
                 bad_sizes_rejected = False
@@ -55,9 +56,12 @@ def _worker(rank, world, port, batch, q):
         ok = (torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5)
               and torch.equal(pooled, pooled2) and torch.equal(out, out2) and proto2.shape[0] == own
               # DataParallel call pattern: pooled / logits cover the whole batch everywhere, the
-              # proto map is gathered to rank 0 (DataParallel's output device), shards elsewhere
+              # proto map is gathered to rank 0 (DataParallel's output device); the other ranks
+              # get None, so proto[i] over the batch cannot silently pick a wrong image there
               and ((proto.shape == r_proto.shape and torch.allclose(proto, r_proto, atol=1e-6)) if rank == 0
-                   else torch.allclose(proto, r_proto[start:start + own], atol=1e-6))
+                   else proto is None)
+              # gather_proto=False keeps each rank's own shard
+              and torch.allclose(proto5, r_proto[start:start + own], atol=1e-6)
               and proto4.shape == r_proto.shape and torch.allclose(proto4, r_proto, atol=1e-6)
               and torch.equal(pooled, pooled3) and torch.equal(out, out3) and bad_sizes_rejected
               and wrapped.module is net)
@@ -86,3 +90,47 @@ def test_shard_sizes_match_torch_chunk():
             ref = [c.shape[0] for c in torch.arange(b).chunk(w)] if b else []
             ref += [0] * (w - len(ref))
             assert shard_sizes(b, w) == ref, (b, w)
+
+
+def _group_worker(rank, world, port, q):
+    """bench.py's C5 layout at N = 8: two independent 4-rank groups (dist.new_group), every rank
+    passing its own shard; each group's gathered outputs equal its own 4-shard batch."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+        from count_pipnet_amd.backend import torch_backend
+        from golden_util import golden_inputs, load_golden
+        from model_util import build_model
+        meta, _ = load_golden("pipnet_mid_addon")
+        net = build_model(meta)
+        base = golden_inputs(meta)
+        groups = [dist.new_group(list(range(g0, g0 + 4))) for g0 in range(0, world, 4)]
+        g = rank // 4
+        # group g's batch: 4 shards of 1 image, image i of group g = base[(g + i) % len(base)] * (1 + g)
+        imgs = torch.stack([base[(g + i) % base.shape[0]] * (1 + 0.1 * g) for i in range(4)])
+        wrapped = ShardedInference(net, process_group=groups[g])
+        with torch.no_grad(), torch_backend():
+            _, pooled, out = wrapped(imgs[rank % 4:rank % 4 + 1], inference=True, global_batch=False,
+                                     sizes=[1] * 4)
+            _, r_pooled, r_out = net(imgs, inference=True)
+        ok = (pooled.shape[0] == 4 and torch.allclose(pooled, r_pooled, atol=1e-6)
+              and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5) and wrapped.world == 4 and wrapped.rank == rank % 4)
+        q.put((rank, bool(ok)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_inference_two_groups_world8():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_group_worker, args=(r, 8, port, q)) for r in range(8)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    res = dict(q.get(timeout=5) for _ in range(8))
+    assert res == {r: True for r in range(8)}

@@ -110,3 +110,55 @@ def test_c5_images_vs_oracle(c5):
     for i in np.nonzero(ok)[0]:
         assert torch.equal(counts[i], r_counts[i])
         assert ((out[i] - r_out[i]).abs() / r_out[i].abs().clamp(min=1)).max().item() <= TOL
+
+
+# ---- the bilinear fold: in-tree fp64 kernel and its cache -------------------------
+
+def test_matmul_f64acc_matches_float64(gpu):
+    """pipnet_matmul_f64acc_f32 (csrc/fold_f64.hip) = float64 matmul rounded to fp32, on ragged
+    shapes (no multiple of the 64 x 64 x 16 tile) and on the C5 fold's own shape."""
+    from count_pipnet_amd import kernels as K
+    g = torch.Generator().manual_seed(7)
+    for m, n, k in [(1, 1, 1), (37, 70, 19), (130, 65, 257), (6144, 2048, 6144)]:
+        a = torch.randn(m, k, generator=g)
+        b = torch.randn(k, n, generator=g)
+        ref = (a.double() @ b.double()).float()
+        out = K.matmul_f64acc(a.to(gpu), b.to(gpu)).cpu()
+        # one fp32 rounding of an fp64 sum: equal except at rounding midpoints (1 ulp)
+        ulp = torch.finfo(torch.float32).eps * ref.abs().clamp_min(1e-30)
+        assert ((out - ref).abs() <= ulp).all(), (m, n, k)
+        assert (out == ref).float().mean() > 0.999, (m, n, k)
+
+
+def test_bilinear_fold_tracks_weight_updates(gpu):
+    """The folded (W E, V E) weights follow every in-place update that bumps a parameter's
+    version (optimizer-style ``copy_``/``add_``, ``load_state_dict``); a ``.data`` write is
+    invisible to the stamp until ``invalidate_weight_caches`` (documented limitation)."""
+    from count_pipnet_amd import invalidate_weight_caches
+    from count_pipnet_amd.count_pipnet import intermediate_hip
+    from count_pipnet_amd.count_pipnet_utils import BilinearIntermediate
+    torch.manual_seed(0)
+    layer = BilinearIntermediate(96, 3, custom_init=True).to(gpu).eval()
+    x = torch.randint(0, 4, (16, 96), device=gpu).float()
+
+    def check():
+        with torch.no_grad():
+            e = x.double() @ layer.embed.weight.double().t()
+            ref = (e @ layer.W.weight.double().t()) * (e @ layer.V.weight.double().t())
+            out = intermediate_hip(layer, x).double()
+        scale = ref.abs().max().item()
+        return (out - ref).abs().max().item() / scale
+
+    with torch.no_grad():
+        assert check() < 1e-5
+        layer.W.weight.add_(0.05 * torch.randn_like(layer.W.weight))          # optimizer-style
+        assert check() < 1e-5
+        sd = {k: v + 0.05 * torch.randn_like(v) for k, v in layer.state_dict().items()}
+        layer.load_state_dict(sd)                                             # checkpoint load
+        assert check() < 1e-5
+        layer.V.weight.copy_(layer.V.weight * 0.5 + 0.01)                     # in-place copy_
+        assert check() < 1e-5
+        layer.embed.weight.data.mul_(1.5)                                     # bypasses _version
+        assert check() > 1e-3                                                 # stale, as documented
+        assert invalidate_weight_caches(layer) >= 1
+        assert check() < 1e-5

@@ -22,6 +22,7 @@ lib.lab_set_stamps.argtypes = [P]
 
 
 def shapes(batch=64):
+    batch *= int(os.environ.get("STAMP_MSCALE", "1"))     # longer dispatches (clock reconciliation)
     out = []
     for d, hw in [(96, 56), (192, 28), (384, 27), (768, 26)]:
         m = batch * hw * hw
@@ -76,7 +77,7 @@ def main():
         per_cu = np.bincount(np.unique(cu, return_inverse=True)[1])
         clk = (a[:, 3] - a[:, 0]).sum() / max(life_rt.sum(), 1) * 100e6
         occ = life_rt.sum() / (span_rt * ncu)
-        print(f"{name:9s} v{v} M={m} N={n} K={k} wg={nwg} nk={nk} CUs={ncu} wg/CU={per_cu.min()}..{per_cu.max()} "
+        print(f"{name:9s} v{v} M={m} N={n} K={k} wg={nwg} grid={nwg * 256} nk={nk} CUs={ncu} wg/CU={per_cu.min()}..{per_cu.max()} "
               f"clk={clk / 1e9:.2f}GHz span={span_rt / 100:.1f}us", flush=True)
         print(f"   cycles median: prologue {np.median(pro):.0f}  main {np.median(main_):.0f} "
               f"({np.median(main_) / nk:.0f}/K-tile)  epilogue {np.median(epi_):.0f} | "
