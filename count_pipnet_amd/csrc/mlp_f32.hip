@@ -54,8 +54,10 @@ struct MlpGeo {
 // NCH/HS) (both parts' chunks staged side by side), the partial out^T summed part 0 + part 1
 // through LDS before the epilogue -- HS x the waves per pixel (C5's stage 2 has 1024 pixel
 // groups: one wave per SIMD at HS = 1).  The hidden order, and so the rounding, depends on HS
-// only (never on M), so a fixed HS per C keeps the results batch-invariant.  The product uses
-// HS = 1 for both C (HS = 2 helps C5's stage 2 but not C2's, profiles/r02/mlp_lab.txt).
+// only (never on M), so choosing HS from the layer alone keeps the results batch-invariant.
+// The product (pipnet_cnblock_mlp_hw_f32) takes HS = 2 for C = 192 on maps of at most
+// MLP_HS2_MAX_HW pixels per image (C5's stage 2 and C1: 16x16 / 8x8 maps) and HS = 1 otherwise
+// (C2's 28x28 stage 2, every C = 96 stage; profiles/r02/mlp_lab.txt, profiles/r03/bench_mlp_hs2.log).
 template <int C, int HC, int NW, int PX, int HS = 1>
 __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,

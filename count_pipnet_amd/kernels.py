@@ -35,8 +35,9 @@ def _launch(kname: str, flops: float, fn) -> None:
 
 
 def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
-    """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant in
-    csrc/gemm_f32.hip; alignment is always satisfied by torch allocations)."""
+    """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant and
+    launch_gemm in csrc/gemm_f32.hip for dense, unit-stride operands: leading dimensions equal
+    to K / N, 16-B aligned torch allocations -- so ``vec_epi`` holds whenever N % 4 == 0)."""
     if k % 16 == 0 and ((k <= 96 and n > 192 and m > 64) or (k % 32 and m > 64)):
         return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if k % 32:
@@ -44,23 +45,26 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     if n <= 384 or k <= 192 or m <= 64:
         npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
-    if aload == 0 and n % 128 == 0 and k >= 256 and epilogue != _lib.EPI_RESID_ROWSCALE \
-            and -(-m // 128) * (n // 128) >= 4 * _num_cus() and gemm_stream():
+    if aload == 0 and n % 128 == 0 and k % 32 == 0 and k >= 256 and epilogue != _lib.EPI_RESID_ROWSCALE \
+            and -(-m // 128) * (n // 128) >= 4 * _num_cus() and max(m * k, n * k, m * n) < 2 ** 31 \
+            and gemm_stream():
         return f"pipnet_gemm::gemm_f32_tn_stream_kernel<{epilogue}>"
     if aload == 0 and n % 128 == 0 and gemm_persist():
         return f"pipnet_gemm::gemm_f32_tn_persist_kernel<{epilogue}>"
     return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
 
 
-_CUS = None
+_CUS = {}
 
 
 def _num_cus() -> int:
-    global _CUS
-    if _CUS is None:
-        _CUS = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count \
-            if torch.cuda.is_available() else 256
-    return _CUS
+    """CUs of the current device (per device, as the library's launch rule sees it)."""
+    if not torch.cuda.is_available():
+        return 256
+    d = torch.cuda.current_device()
+    if d not in _CUS:
+        _CUS[d] = torch.cuda.get_device_properties(d).multi_processor_count
+    return _CUS[d]
 
 
 def gemm_stream(mode: int = -1) -> bool:

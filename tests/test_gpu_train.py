@@ -358,6 +358,36 @@ def _optimizers_like_reference(net, meta, fwd_meta):
 
 
 @pytest.mark.parametrize("name", SUFFIX)
+def _resnet_first_grads_close(net, rec):
+    """the AdamW trajectory bound is sign-like (it cannot see a right-sign gradient of
+    the wrong magnitude), so pin the magnitude directly: the HIP gradients of iteration 0 -- the
+    same weights the reference differentiated -- against the reference's recorded ones, per
+    trainable tensor: norm ratio within 10 %, and every element within 25 % of max|g| (whole
+    ResNet-50 backprop in fp32 lands 2-3 % from fp64 in the median for torch as well,
+    tools/resnet_grad_conditioning.py)."""
+    params = dict(net.named_parameters())
+    checked = 0
+    for key in rec:
+        if not key.startswith("grad0/"):
+            continue
+        pname = key.split("/", 1)[1]
+        p = params.get(pname)
+        if p is None or p.grad is None:
+            continue
+        g_ref = _t(rec[key]).double().flatten()
+        g_hip = p.grad.detach().cpu().double().flatten()[:g_ref.numel()]
+        g_ref = g_ref[:g_hip.numel()]
+        scale = g_ref.abs().max().item()
+        if scale == 0.0:
+            continue
+        ratio = g_hip.norm().item() / max(g_ref.norm().item(), 1e-30)
+        assert 0.9 <= ratio <= 1.1, f"{pname}: |g_hip| / |g_ref| = {ratio:.4f}"
+        err = (g_hip - g_ref).abs().max().item() / scale
+        assert err <= 0.25, f"{pname}: max |g_hip - g_ref| = {err:.3f} of max|g|"
+        checked += 1
+    assert checked > 0
+
+
 def test_suffix_training_matches_reference(gpu, name):
     meta, rec, fwd_meta = load_train_golden(name)
     net = build_model(fwd_meta).to(gpu).train()
@@ -374,6 +404,8 @@ def test_suffix_training_matches_reference(gpu, name):
         opt_cls.zero_grad(set_to_none=True)
         stats = T.hip_train_step(net, xs1.to(gpu), xs2.to(gpu), ys.to(gpu), opt_net, opt_cls, pretrain, 1,
                                  2 if pretrain else 1, True, sd_keep=sd_keep).cpu()
+        if i == 0 and fwd_meta["case"]["net"].startswith("resnet"):
+            _resnet_first_grads_close(net, rec)
         comp = meta["components"][i]
         assert float(stats[0]) == pytest.approx(comp["align"], rel=2e-3, abs=1e-4)
         assert float(stats[1]) == pytest.approx(comp["tanh"], rel=2e-3, abs=1e-4)
