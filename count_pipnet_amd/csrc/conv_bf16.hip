@@ -1,6 +1,8 @@
 // bf16 ResNet path (BASELINE C3): implicit-GEMM convolution (gemm_bf16_impl.hpp), NCHW fp32
 // -> NHWC bf16 input relayout, NHWC bf16 max-pool.  Reference: features/resnet_features.py
 // (conv / BatchNorm / ReLU / Bottleneck / MaxPool2d, :77-229).
+#include <cstdlib>
+
 #include "gemm_bf16_impl.hpp"
 
 using namespace pipnet_bf16;
@@ -86,7 +88,8 @@ bool halo64_ok(const ConvParams& p, int epi) {
 
 bool halo_ok(const ConvParams& p, int epi) {
   return p.KW == 3 && p.Kv == 9 * p.Cin && p.stride == 1 && p.pad == 1 && p.OH == p.H && p.OW == p.Wd &&
-         p.seg == 0 && p.Cin % 64 == 0 && p.Wd <= 31 && p.N >= 256 && !is_s3_epi(epi);
+         p.seg == 0 && p.Cin % 64 == 0 && p.Wd <= 31 && p.N >= 256 && !is_s3_epi(epi) &&
+         (int64_t)p.M * p.Cin < ((int64_t)1 << 31);        // 32-bit halo source offsets
 }
 // B fragments of 16 columns per wave.  Only the 256-wide tile is dispatched: the 64 / 128-wide
 // instantiations (4 / 8 MFMAs per phase) measured slower than tile 6 on layer1 conv2 (125 vs
@@ -97,6 +100,35 @@ bool halo_ok(const ConvParams& p, int epi) {
 #define H64_AUTO 1
 #endif
 int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
+
+// Row blocks per wave group of the 256-wide ping-pong tiles (halo 8, persistent 9): 8 -> 256-row
+// tiles, 7 -> 224-row tiles.  C3's layers have M = 784 per image, so at 64 images 196 row tiles
+// of 256 leave 60 CUs idle (N = 256) or a half-empty last round (N = 512: 392 tiles = 1.53
+// rounds); 224 rows give 224 / 448 tiles (0.875 / 1.75 rounds).  Cost model: rounds of tiles x
+// tile work, a 224-row tile charged 7/8 of a 256-row one plus 3 % (B is fetched whole for 7/8 of
+// the rows).  Every output element is the same MFMA chain over the same K order in both forms,
+// so this M-dependent choice keeps every pixel's bits batch-invariant.  Mirrored by
+// kernels.py:bf16_pp_rb.  pipnet_conv_bf16_rb (or PIPNET_PP_RB=7/8 in the environment) forces one
+// form, for tests and A/B runs.
+int g_pp_rb = -1;
+int pp_rb_mode() {
+  if (g_pp_rb < 0) {
+    const char* e = getenv("PIPNET_PP_RB");
+    const int v = e ? atoi(e) : 0;
+    g_pp_rb = (v == 7 || v == 8) ? v : 0;
+  }
+  return g_pp_rb;
+}
+int pick_rb(int M, int nt) {
+  const int forced = pp_rb_mode();
+  if (forced == 7 || forced == 8) return forced;
+  const int64_t ncu = num_cus();
+  auto cost = [&](int rb) {
+    const int64_t tiles = (int64_t)((M + 32 * rb - 1) / (32 * rb)) * nt;
+    return (double)((tiles + ncu - 1) / ncu) * (rb == 8 ? 1.0 : 0.875 * 1.03);
+  };
+  return cost(7) < cost(8) ? 7 : 8;
+}
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
@@ -140,24 +172,25 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   }
   if (v == 9) {                                  // persistent 256 x 256 ping-pong (1x1, N % 256 == 0)
     p.nt = p.N / 256;
-    p.mt = (p.M + 255) / 256;
+    const int rb = pick_rb(p.M, p.nt);
+    p.mt = (p.M + 32 * rb - 1) / (32 * rb);
     p.group_m = choose_group_m(p.K);
     const int ntiles = p.mt * p.nt;
     const dim3 grid(ntiles < num_cus() ? ntiles : num_cus());
+#define PIPNET_PPP(E)                                                                                  \
+  case E:                                                                                               \
+    if (rb == 7) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 7>), grid, dim3(512), 0, s, p);           \
+    else hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 8>), grid, dim3(512), 0, s, p);                   \
+    break;
     switch (epi) {
-      case PIPNET_EPI_NONE: hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_NONE>), grid, dim3(512), 0, s, p); break;
-      case PIPNET_EPI_BIAS: hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS>), grid, dim3(512), 0, s, p); break;
-      case PIPNET_EPI_BIAS_RELU:
-        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS_RELU>), grid, dim3(512), 0, s, p);
-        break;
-      case PIPNET_EPI_BIAS_RESID_RELU:
-        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_BIAS_RESID_RELU>), grid, dim3(512), 0, s, p);
-        break;
-      case PIPNET_EPI_DUAL_BIAS_RELU:
-        hipLaunchKernelGGL((conv_bf16_ppp_kernel<PIPNET_EPI_DUAL_BIAS_RELU>), grid, dim3(512), 0, s, p);
-        break;
+      PIPNET_PPP(PIPNET_EPI_NONE)
+      PIPNET_PPP(PIPNET_EPI_BIAS)
+      PIPNET_PPP(PIPNET_EPI_BIAS_RELU)
+      PIPNET_PPP(PIPNET_EPI_BIAS_RESID_RELU)
+      PIPNET_PPP(PIPNET_EPI_DUAL_BIAS_RELU)
       default: return PIPNET_ERR_ARG;
     }
+#undef PIPNET_PPP
     PIPNET_CHECK_LAUNCH();
     return PIPNET_OK;
   }
@@ -165,12 +198,14 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   if (v == 8) {                                  // ping-pong with the LDS input halo, 256 x 64 NB
     const int nb = halo_nb(p.N);
     p.nt = (p.N + 64 * nb - 1) / (64 * nb);
-    p.mt = (p.M + 255) / 256;
+    const int rb = nb == 4 ? pick_rb(p.M, p.nt) : 8;
+    p.mt = (p.M + 32 * rb - 1) / (32 * rb);
     p.group_m = choose_group_m(p.K);
     const dim3 grid(p.mt * p.nt);
 #define PIPNET_HALO(E)                                                                                \
   case E:                                                                                              \
-    if (nb == 4) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4>), grid, dim3(512), 0, s, p);       \
+    if (nb == 4 && rb == 7) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4, 7>), grid, dim3(512), 0, s, p); \
+    else if (nb == 4) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4, 8>), grid, dim3(512), 0, s, p); \
     else return PIPNET_ERR_ARG;                                                                        \
     break;
     switch (epi) {
@@ -396,6 +431,12 @@ extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int C
                                        const void* R, int epilogue, void* y, void* stream) {
   return pipnet_conv2d_nhwc_bf16_tile(x, B, H, W, Cin, w_packed, bias, Cout, KH, KW, stride, pad, R, epilogue, y, -1,
                                       stream);
+}
+
+extern "C" int pipnet_conv_bf16_rb(int mode) {
+  if (mode == 0 || mode == 7 || mode == 8) g_pp_rb = mode;
+  else if (mode != -1) return -PIPNET_ERR_ARG;
+  return pp_rb_mode();
 }
 
 extern "C" int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias,

@@ -457,10 +457,14 @@ template <int NPEND>
 PIPNET_DEV void pp_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPEND) : "memory");
 }
-// runtime (wave-uniform) count -> immediate: the counts are even and <= 4 DB - 2
+// runtime (wave-uniform) count -> immediate: the counts are <= 4 DB - 2 (odd ones from the
+// one-A-piece waves of 224-row persistent tiles)
 PIPNET_DEV void pp_wait_vm_dyn(int n) {
   switch (n) {
     case 0: pp_wait_vm<0>(); break;
+    case 1: pp_wait_vm<1>(); break;
+    case 3: pp_wait_vm<3>(); break;
+    case 5: pp_wait_vm<5>(); break;
     case 2: pp_wait_vm<2>(); break;
     case 4: pp_wait_vm<4>(); break;
     case 6: pp_wait_vm<6>(); break;
@@ -478,11 +482,15 @@ PIPNET_DEV void pp_barrier() {
 // re-laid through its own LDS rows (64 x 68 floats), then every lane finishes 8 consecutive
 // channels of one pixel (bias, residual, ReLU or the split-bf16 forms) with 16-B accesses.
 // The stage buffers must be free (all waves past the main loop's last barrier).
-template <int EPI, int NB>
+// RB = 16-row blocks per wave group (8: 256-row tiles; 7: 224-row tiles, see conv_bf16.hip
+// pick_rb): half 0 holds blocks 0..3, half 1 blocks 4..RB-1.
+template <int EPI, int NB, int RB = 8>
 PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], unsigned char* smem, int m0, int n0,
                             int wr, int wc, int lane, int wid) {
   using namespace pp;
+  static_assert(RB == 7 || RB == 8, "RB");
   constexpr int WCOLS = 16 * NB;
+  const int mw = m0 + wr * 16 * RB;              // first row of this wave group
   const int fr = lane & 15;
   constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
   float* wt = reinterpret_cast<float*>(smem) + wid * 64 * EPI_LD;
@@ -504,16 +512,17 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int m = min(m0 + wr * 128 + half * 64 + it * 8 + (lane >> 3), p.M - 1);
+      for (int it = 0; it < 2 * (half ? RB - 4 : 4); ++it) {
+        const int m = min(mw + half * 64 + it * 8 + (lane >> 3), p.M - 1);
         if (nok) rrs[half][it] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
       }
   }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
+    const int nr = half ? RB - 4 : 4;            // row blocks of this half (compile-time after unrolling)
     bf16x8v (&rr)[8] = rrs[half];
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
+    for (int r = 0; r < nr; ++r)
 #pragma unroll
       for (int nn = 0; nn < NB; ++nn)
 #pragma unroll
@@ -521,9 +530,9 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
           wt[(r * 16 + 4 * (lane >> 4) + i) * EPI_LD + nn * 16 + fr] = acc[half * 4 + r][nn][i];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 2 * nr; ++it) {
       const int row = it * 8 + (lane >> 3);
-      const int m = m0 + wr * 128 + half * 64 + row;
+      const int m = mw + half * 64 + row;
       f32x4v x0 = *reinterpret_cast<const f32x4v*>(wt + row * EPI_LD + 8 * c8);
       f32x4v x1 = *reinterpret_cast<const f32x4v*>(wt + row * EPI_LD + 8 * c8 + 4);
       x0 += b0;
@@ -761,7 +770,6 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 namespace ppp {
 constexpr int OFF_EPI = 4 * pp::STAGE_BYTES;          // 128 KiB of stages (DB = 2), then 8 x 4 KiB
 constexpr int SMEM = OFF_EPI + 8 * 16 * 64 * 4;
-constexpr int NSTORE = 16;                            // epilogue 16-B stores per lane per tile
 PIPNET_DEV int swz(int r) { return (((r >> 2) & 3) << 4) | ((r & 1) << 2); }
 }  // namespace ppp
 
@@ -777,10 +785,17 @@ PIPNET_DEV void tile_coords_id(const ConvParams& p, int id, int bm, int bn, int&
   n0 = (in_group / gsz) * bn;
 }
 
-template <int EPI>
+// RB = 16-row blocks per wave group: 8 -> 256-row tiles, 7 -> 224-row tiles (conv_bf16.hip
+// pick_rb: fewer idle CUs in the last round; bitwise the same outputs).  With RB = 7 the A tile
+// is 14 DMA pieces of 16 rows: waves 0-5 issue two per K-tile, waves 6-7 one (na), and every
+// counted wait uses the wave's own count.
+template <int EPI, int RB = 8>
 __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) {
   using namespace pp;
   constexpr int DB = 2, NS = 4;
+  static_assert(RB == 7 || RB == 8, "RB");
+  constexpr int BMR = 32 * RB;                         // tile rows
+  constexpr int NSTORE = 2 * RB;                       // epilogue 16-B stores per lane per tile
   constexpr bool HAS_R = EPI == PIPNET_EPI_BIAS_RESID_RELU;
   __shared__ __attribute__((aligned(16))) unsigned char smem[ppp::SMEM];
   const int tid = threadIdx.x;
@@ -792,25 +807,27 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 
   const int drow = lane >> 2;
   const int dchunk = 8 * ((lane & 3) ^ g(drow));
+  // A pieces of this wave (wave-uniform): 2, or 1 for waves 6-7 of a 224-row tile
+  const int na = __builtin_amdgcn_readfirstlane(wid + 8 < 2 * RB ? 2 : 1);
   int64_t abase[2];
   const bf16* wsrc[2];
   auto setup = [&](int id, int& m0, int& n0) {
-    tile_coords_id(p, id, BM, BN, m0, n0);
+    tile_coords_id(p, id, BMR, BN, m0, n0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int row = 16 * (wid + 8 * i) + drow;
-      abase[i] = (int64_t)min(m0 + row, p.M - 1) * p.lda + dchunk;
+      abase[i] = (int64_t)min(m0 + min(row, BMR - 1), p.M - 1) * p.lda + dchunk;
       wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
     }
   };
   auto stage_a = [&](int kt) {
     unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
     const int k0 = seg_remap(p, min(kt * BK, p.Kv - BK));
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + abase[i] + k0),
-                                       (__attribute__((address_space(3))) void*)(base + (wid + 8 * i) * 1024), 16,
-                                       0, 0);
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + abase[0] + k0),
+                                     (__attribute__((address_space(3))) void*)(base + wid * 1024), 16, 0, 0);
+    if (RB == 8 || na == 2)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(p.A + abase[1] + k0),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + 8) * 1024), 16, 0, 0);
   };
   auto stage_b = [&](int kt) {
     unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
@@ -830,15 +847,22 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
   const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
   auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* st, int half) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + half * 64 + r * 16) * ROWB + fofs);
+    for (int r = 0; r < (half ? RB - 4 : 4); ++r)
+      fa[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 16 * RB + half * 64 + r * 16) * ROWB + fofs);
   };
   auto read_b = [&](bf16x8v (&fb)[4], const unsigned char* st) {
 #pragma unroll
     for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 64 + n * 16) * ROWB + fofs);
   };
+  // this wave's pieces issued after its B(kt + 1): A(kt+2), B(kt+2), A(kt+3), those that exist
   auto younger_than_b = [&](int kt) {
-    return ((kt + 2 < nk) ? 4 : 0) + ((kt + 3 < nk) ? 2 : 0);
+    return ((kt + 2 < nk) ? 2 + na : 0) + ((kt + 3 < nk) ? na : 0);
+  };
+  // the steady-state wait (2 + 2 na pieces younger than B(kt + 1)), as an immediate
+  auto wait_steady = [&](auto extra) {
+    constexpr int X = decltype(extra)::value;
+    if (RB == 8 || na == 2) pp_wait_vm<6 + X>();
+    else pp_wait_vm<4 + X>();
   };
 
   int m0, n0;
@@ -872,12 +896,12 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       pp_barrier();
       if (STEADY || kt + DB + 1 < nk) stage_a(kt + DB + 1);
       read_a(fa, st, 1);
-      if constexpr (STEADY) pp_wait_vm<6>();
+      if constexpr (STEADY) wait_steady(IntC<0>{});
       else pp_wait_vm_dyn(younger_than_b(kt));
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < RB - 4; ++r)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
           acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
@@ -900,11 +924,11 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       pp_barrier();
       stage_a(DB + 1);
       read_a(fa, st, 1);
-      pp_wait_vm<6 + ppp::NSTORE>();
+      wait_steady(IntC<NSTORE>{});
       pp_barrier();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < RB - 4; ++r)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
           acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
@@ -946,15 +970,15 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     bf16x8v rr[16];
     if (HAS_R) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = min(cm0 + wr * 128 + q * 8 + (lane >> 3), p.M - 1);
+      for (int q = 0; q < 2 * RB; ++q) {
+        const int m = min(cm0 + wr * 16 * RB + q * 8 + (lane >> 3), p.M - 1);
         rr[q] = __builtin_bit_cast(bf16x8v, __builtin_nontemporal_load(
                     reinterpret_cast<const u32x4*>(p.R + (int64_t)m * p.ldr + n)));   // read once
       }
     }
     const int fq = lane >> 4;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
+    for (int r = 0; r < RB; ++r) {
 #pragma unroll
       for (int nn = 0; nn < 4; ++nn)
 #pragma unroll
@@ -991,7 +1015,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
           o[e] = (bf16)x0[e];
           o[4 + e] = (bf16)x1[e];
         }
-        const int m = min(cm0 + wr * 128 + r * 16 + row, p.M - 1);
+        const int m = min(cm0 + wr * 16 * RB + r * 16 + row, p.M - 1);
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(cout + (int64_t)m * ldo + no));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -999,8 +1023,8 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     if (!more) break;
     // next tile's A(0) / B(0): younger are A1 B1 A2 (6) and this epilogue's stores (and, with a
     // residual, its loads -- already consumed, hence retired with everything older)
-    if (nk > 2) pp_wait_vm<6 + ppp::NSTORE>();
-    else pp_wait_vm<ppp::NSTORE>();    // fewer than 6 pieces follow B(0): wait a little longer
+    if (nk > 2) wait_steady(IntC<NSTORE>{});
+    else pp_wait_vm<NSTORE>();         // fewer pieces follow B(0): wait a little longer
     pp_barrier();
     extra = 1;
   }
@@ -1059,11 +1083,16 @@ struct Lay {
 };
 }  // namespace ph
 
-template <int EPI, int NB = 4>
+// RB = 16-row blocks per wave group: 8 -> 256-row tiles, 7 -> 224-row tiles (fewer idle CUs in
+// the last round of tiles, conv_bf16.hip pick_rb).  Every output element is the same MFMA chain
+// over the same K order whatever RB is, so the choice never changes a bit of the result.
+template <int EPI, int NB = 4, int RB = 8>
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
   using namespace pp;
   using ph::NS;
   using L = ph::Lay<NB>;
+  static_assert(RB == 7 || RB == 8, "RB");
+  constexpr int BMR = 32 * RB;                                 // tile rows
   // The 64 / 128-wide forms (NB = 1 / 2: 384-row halo, duplicated B pieces) passed the
   // kernel-level tests but measured slower / flat and failed the C3 end-to-end bf16 bound
   // (pooled 0.10 vs 0.05) in their one run -- not dispatched, not validated.
@@ -1075,7 +1104,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   const int wid = tid >> 6;
   const int wr = wid >> 2, wc = wid & 3;
   int m0, n0;
-  tile_coords(p, BM, L::BROWS, m0, n0);
+  tile_coords(p, BMR, L::BROWS, m0, n0);
   const int W = p.Wd, HW = p.H * p.Wd;
   const int npair = p.Cin / (2 * BK);
   const int nk = 18 * npair;
@@ -1093,25 +1122,26 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   }
   int bdst[L::BPW];
 #pragma unroll
-  for (int i = 0; i < L::BPW; ++i) bdst[i] = (L::BROWS / 16 >= 8 ? wid + 8 * i : (wid % (L::BROWS / 16))) * 1024;
+  for (int i = 0; i < L::BPW; ++i)    // wave-uniform: SGPRs (as VGPRs they pushed the RB = 8 form into spills)
+    bdst[i] = __builtin_amdgcn_readfirstlane((L::BROWS / 16 >= 8 ? wid + 8 * i : (wid % (L::BROWS / 16))) * 1024);
   // ---- halo DMA: 2 HPC pieces per pair, HPW per wave: piece e = wid + 8 i is chunk half
   // e / HPC, halo rows 16 (e % HPC) + ...; halo row i = pixel m0 - W - 1 + i ----
-  int64_t hsrc[L::HPW];
+  int hsrc[L::HPW];                                           // element offsets: M * Cin < 2^31 (halo_ok)
   int hdst[L::HPW];
 #pragma unroll
   for (int i = 0; i < L::HPW; ++i) {
     const int e = wid + 8 * i, h = e >= L::HPC ? 1 : 0, pc = e - L::HPC * h;
     const int row = 16 * pc + drow;
     const int pix = min(max(m0 - W - 1 + row, 0), p.M - 1);
-    hsrc[i] = (int64_t)pix * p.Cin + h * BK + 8 * ((lane & 3) ^ ph::hs(row));
-    hdst[i] = h * L::HALO_BYTES + pc * 1024;
+    hsrc[i] = pix * p.Cin + h * BK + 8 * ((lane & 3) ^ ph::hs(row));
+    hdst[i] = __builtin_amdgcn_readfirstlane(h * L::HALO_BYTES + pc * 1024);
   }
   // ---- this lane's 8 fragment rows: tile row wr*128 + j*16 + (lane & 15); 9-bit tap masks ----
   const int fr = lane & 15;
   unsigned vmask[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int m = m0 + wr * 128 + j * 16 + fr;
+    const int m = m0 + wr * 16 * RB + j * 16 + fr;
     unsigned mk = 0;
     if (m < p.M) {
       const int rr = m % HW;
@@ -1155,7 +1185,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* hb, int half, int loff, unsigned tbit) {
     const unsigned char* zl = zb + (loff & 255);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < (half ? RB - 4 : 4); ++r) {
       const int j = half * 4 + r;
       const unsigned char* ptr = (vmask[j] & tbit) ? hb + loff + j * 1024 : zl;
       fa[r] = *reinterpret_cast<const bf16x8v*>(ptr);
@@ -1184,7 +1214,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   // in the last tap of the last pair.  Everything but the MFMA stream is scalar bookkeeping
   // kept branch-light (one compile-time h per unrolled half).
   bf16x8v fa[4], fb[NB];
-  const int lrow = wr * 128 + fr;
+  const int lrow = wr * 16 * RB + fr;
   int kt = 0;
   for (int P = 0; P < npair; ++P) {
     const bool more = P + 1 < npair;
@@ -1221,7 +1251,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
         pp_barrier();
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int r = 0; r < RB - 4; ++r)
 #pragma unroll
           for (int n = 0; n < NB; ++n)
             acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
@@ -1233,7 +1263,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   if (wr == 0) pp_barrier();                                   // re-align the groups
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pp_barrier();                                                // stage / halo buffers free for the epilogue
-  pp_epilogue<EPI, NB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
+  pp_epilogue<EPI, NB, RB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
 }
 
 // ======================================================================================

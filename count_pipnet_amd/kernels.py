@@ -287,6 +287,30 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
              4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2), 6: ("pipnet_bf16::Cfg<4, 1, 2, 2, 32, 4>", 2)}
 
 
+def conv_bf16_rb(mode: int = -1) -> int:
+    """The library's row-block switch of the 256-wide bf16 ping-pong tiles (include/pipnet_amd.h
+    pipnet_conv_bf16_rb): 7 / 8 force 224- / 256-row tiles, 0 = automatic, -1 queries."""
+    r = _lib.load().pipnet_conv_bf16_rb(mode)
+    if r < 0:
+        _lib.check(-r, f"pipnet_conv_bf16_rb({mode})")
+    return r
+
+
+def bf16_pp_rb(m: int, nt: int) -> int:
+    """Row blocks per wave group the library picks for a halo / persistent tile grid of ``nt``
+    256-wide column tiles (mirrors pick_rb in csrc/conv_bf16.hip): 7 (224-row tiles) when that
+    gives fewer tile rounds x tile work per CU, else 8 (256-row tiles)."""
+    mode = conv_bf16_rb(-1) if torch.cuda.is_available() else 0
+    if mode in (7, 8):
+        return mode
+    cus = _num_cus()
+
+    def cost(rb):
+        tiles = -(-m // (32 * rb)) * nt
+        return -(-tiles // cus) * (1.0 if rb == 8 else 0.875 * 1.03)
+    return 7 if cost(7) < cost(8) else 8
+
+
 def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True,
                           s3: bool = False, kv: int = 0, halo_ok: bool = False, ppp_ok: bool = False,
                           halo64_ok: bool = False) -> str:
@@ -295,10 +319,11 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
-        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}>"
+        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}>"
     if t == 8:
         nb = 4 if n >= 256 else (2 if n >= 128 else 1)
-        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, {nb}>"
+        rb = bf16_pp_rb(m, -(-n // (64 * nb))) if nb == 4 else 8
+        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, {nb}, {rb}>"
     if t == 5:
         return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4, 0, 2>"
     if t == 7:
@@ -411,7 +436,7 @@ def conv1x1_bf16_dual(x: Tensor, w_packed: Tensor, bias: Tensor, n1: int, n2: in
     y1 = torch.empty((b, h, w, n1), device=x.device, dtype=torch.bfloat16)
     y2 = torch.empty((b, h, w, n2), device=x.device, dtype=torch.bfloat16)
     m = b * h * w
-    _launch("pipnet_bf16::conv_bf16_ppp_kernel<12>", 2.0 * m * (n1 + n2) * cin,
+    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}>", 2.0 * m * (n1 + n2) * cin,
             lambda: _lib.call("pipnet_conv1x1_bf16_dual", x.data_ptr(), m, cin, w_packed.data_ptr(), bias.data_ptr(),
                               n1, y1.data_ptr(), n2, y2.data_ptr(), _stream(x)))
     return y1, y2

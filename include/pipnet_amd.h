@@ -468,6 +468,14 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
                               float w_align, float w_tanh, float tanh_coeff, float inv_tau, float* dcnt_ws,
                               float* d_logits, void* stream);
 
+/* Row blocks of the 256-wide bf16 ping-pong tiles (the LDS-halo 3x3 tile and the persistent 1x1
+ * tile): mode 7 forces 224-row tiles, 8 forces 256-row tiles, 0 restores the automatic choice
+ * (the form with fewer tile rounds per CU, conv_bf16.hip pick_rb; initially PIPNET_PP_RB from the
+ * environment), -1 queries.  Returns the mode in force or a negative status.  Both forms compute
+ * every output element with the same MFMA chain over the same K order: bitwise equal outputs.
+ * Process-wide A/B switch, not thread-safe against concurrent launches. */
+int pipnet_conv_bf16_rb(int mode);
+
 /* fp64-accumulated product for inference-time weight folds (csrc/fold_f64.hip):
  *   C[M,N] (ldc) = RNE_f32( sum_k double(A[m,k]) * double(B[k,n]) ), A [M,K] (lda) and B [K,N]
  *   (ldb) row-major fp32, products and sums in fp64 on v_mfma_f64_16x16x4_f64, any sizes.

@@ -450,3 +450,54 @@ def test_c3_bf16_full_batch_properties(gpu):
     r_raw, r_out = _fp32_oracle_head(xs[pick].cpu(), sd, args)
     got = _check_bf16_vs_fp32(ipooled[pick].cpu(), iout[pick].cpu(), r_raw, r_out, min_decisive=1)
     print("C3 bs=128 sample bf16 budget:", got)
+
+
+@pytest.mark.parametrize("kind,m_or_b,cin,cout,epi", [
+    ("1x1", 2352, 256, 256, _lib.EPI_BIAS_RELU),            # 3 images of 28x28: ragged for 224 and 256
+    ("1x1", 50176, 1024, 256, _lib.EPI_BIAS_RELU),          # C3 l3.c1 at 64 images (224 / 196 row tiles)
+    ("1x1", 5000, 256, 1024, _lib.EPI_BIAS_RESID_RELU),     # conv3 + identity, ragged
+    ("1x1", 777, 512, 512, _lib.EPI_BIAS),
+    ("1x1", 300, 128, 256, _lib.EPI_NONE),                  # a single, partial 224-row tile
+    ("3x3", 3, 256, 256, _lib.EPI_BIAS_RELU),
+    ("3x3", 5, 512, 512, _lib.EPI_BIAS_RESID_RELU),
+    ("3x3", 2, 256, 512, _lib.EPI_BIAS),
+    ("dual", 4704, 512, (1024, 256), None)])
+def test_pp_tiles_224_rows_bitwise(gpu, kind, m_or_b, cin, cout, epi):
+    """224-row forms (RB = 7) of the persistent 1x1 tile, the LDS-halo 3x3 tile and the dual 1x1
+    launch give bit for bit the 256-row forms' outputs (same MFMA chain and K order per element;
+    the automatic choice between them depends on M, so batch invariance rests on this); ragged M,
+    every epilogue, the one-A-piece waves' counted waits and the halo image borders."""
+    g = torch.Generator().manual_seed(m_or_b + cin)
+    outs = {}
+    try:
+        for rb in (8, 7):
+            assert K.conv_bf16_rb(rb) == rb
+            if kind == "dual":
+                n1, n2 = cout
+                x = torch.randn(1, m_or_b, 1, cin, generator=torch.Generator().manual_seed(1)).to(torch.bfloat16)
+                w = (torch.randn(n1 + n2, 1, 1, cin, generator=torch.Generator().manual_seed(2)) * 0.05)
+                b = torch.randn(n1 + n2, generator=torch.Generator().manual_seed(3))
+                outs[rb] = K.conv1x1_bf16_dual(x.to(gpu), K.pack_conv_weight_bf16(w.to(gpu)), b.to(gpu), n1, n2)
+                continue
+            gg = torch.Generator().manual_seed(7)
+            if kind == "1x1":
+                x = torch.randn(1, m_or_b, 1, cin, generator=gg).to(torch.bfloat16)
+                w = torch.randn(cout, 1, 1, cin, generator=gg) / cin ** 0.5
+                r = torch.randn(1, m_or_b, 1, cout, generator=gg).to(torch.bfloat16)
+                kk, pad = 1, 0
+            else:
+                x = torch.randn(m_or_b, 28, 28, cin, generator=gg).to(torch.bfloat16)
+                w = torch.randn(cout, 3, 3, cin, generator=gg) / (3 * cin ** 0.5)
+                r = torch.randn(m_or_b, 28, 28, cout, generator=gg).to(torch.bfloat16)
+                kk, pad = 3, 1
+            b = torch.randn(cout, generator=gg)
+            out = K.conv2d_nhwc_bf16(x.to(gpu), K.pack_conv_weight_bf16(w.to(gpu)), kk, kk,
+                                     None if epi == _lib.EPI_NONE else b.to(gpu), 1, pad, epi,
+                                     r.to(gpu) if epi == _lib.EPI_BIAS_RESID_RELU else None)
+            outs[rb] = (out,)
+        torch.cuda.synchronize()
+    finally:
+        K.conv_bf16_rb(0)
+    for a, b_ in zip(outs[8], outs[7]):
+        assert torch.equal(a, b_)
+    assert K.conv_bf16_rb(-1) == 0

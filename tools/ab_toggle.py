@@ -2,7 +2,9 @@
 (cdna_hip_programming.md rule 24): rounds of (off, on) timings of net(xs, inference=True).
 
     python tools/ab_toggle.py <module>.<FLAG> <config> [--rounds 5] [--steps 10]
-e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3"""
+e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3
+A library switch function instead of a module flag: fn:<module>.<func>:<off arg>:<on arg>,
+e.g. fn:count_pipnet_amd.kernels.conv_bf16_rb:8:0 (256-row tiles vs the automatic choice)."""
 import argparse
 import importlib
 import json
@@ -25,8 +27,19 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--stream-split", type=int, default=0, help="0 = the model's default")
     a = ap.parse_args()
-    modname, attr = a.flag.rsplit(".", 1)
-    mod = importlib.import_module(modname)
+    if a.flag.startswith("fn:"):
+        _, path, off, on = a.flag.split(":")
+        modname, fname = path.rsplit(".", 1)
+        fn = getattr(importlib.import_module(modname), fname)
+
+        def switch(val):
+            fn(int(on if val else off))
+    else:
+        modname, attr = a.flag.rsplit(".", 1)
+        mod = importlib.import_module(modname)
+
+        def switch(val):
+            setattr(mod, attr, val)
     dev = torch.device("cuda:0")
     cfg = bc.CONFIGS[a.config]
     net = bc.make(cfg, dev)
@@ -39,7 +52,7 @@ def main():
     with torch.no_grad():
         for r in range(a.rounds):
             for val in (False, True):
-                setattr(mod, attr, val)
+                switch(val)
                 for _ in range(2):
                     o = net(xs, inference=True)
                 torch.cuda.synchronize()

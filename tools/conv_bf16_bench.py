@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None, help="comma-separated layer names")
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5")
+    ap.add_argument("--rb-ab", action="store_true",
+                    help="time the automatic tile twice: 256-row ping-pong tiles forced (r8) and the automatic "
+                         "224/256-row choice (rA) -- kernels.conv_bf16_rb")
     ap.add_argument("--lib", action="store_true",
                     help="also time the vendor library on the same shape (torch bf16: hipBLASLt GEMM for 1x1 "
                          "convs, MIOpen channels_last conv otherwise) as a reference ceiling")
@@ -48,6 +51,8 @@ def main():
     build.build()
     dev = torch.device("cuda:0")
     tiles = [int(t) for t in a.tiles.split(',')]
+    if a.rb_ab:
+        tiles = ["r8", "rA"]
     total = {t: 0.0 for t in tiles}
     for name, h, cin, cout, k, s, pad, epi, cnt in LAYERS:
         if a.only and name not in a.only.split(","):
@@ -64,9 +69,12 @@ def main():
         auto = K.bf16_conv_tile(a.batch * oh * oh, cout, kv=k * k * cin, halo_ok=halo, ppp_ok=ppp, halo64_ok=h64)
         line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={auto}"
         for t in tiles:
+            if isinstance(t, str):          # --rb-ab: automatic tile, row-block mode r8 / rA
+                K.conv_bf16_rb(8 if t == "r8" else 0)
+            ti = -1 if isinstance(t, str) else t
             try:
                 for _ in range(2):
-                    K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=t)
+                    K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=ti)
             except RuntimeError:          # tile not applicable to this layer (e.g. 5 on the Cin=8 stem)
                 line += f"  t{t}:    n/a"
                 total[t] += float("nan")
@@ -74,7 +82,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.reps):
-                K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=t)
+                K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=ti)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.reps

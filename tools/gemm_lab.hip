@@ -79,6 +79,7 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 42: launch<32, 1, 3, 2, 0, 1>(p, epi, s); break;
     case 41: launch<32, 1, 2, 2, 0, 1>(p, epi, s); break;
     case 70: launch<32, 2, 2, 2, 8, 1>(p, epi, s); break;
+    case 37: launch<16, 2, 3, 3, 8>(p, epi, s); break;    // v7 with stamps
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;

@@ -48,6 +48,8 @@ def main():
         if only and name not in only:
             continue
         v, bm, bk = variant_for(m, n, k)
+        if os.environ.get("STAMP_VAR"):            # e.g. 37 = the 3-workgroup BK16 tile (lab v7)
+            v, bm, bk = int(os.environ["STAMP_VAR"]), 128, 16
         if os.environ.get("STAMP_V16") == "1" and v == 30:
             v = 70                      # the same tile on v_mfma_f32_16x16x4_f32
         mt, nt = -(-m // bm), -(-n // 128)
