@@ -110,18 +110,26 @@ int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
 // so this M-dependent choice keeps every pixel's bits batch-invariant.  Mirrored by
 // kernels.py:bf16_pp_rb.  pipnet_conv_bf16_rb (or PIPNET_PP_RB=7/8 in the environment) forces one
 // form, for tests and A/B runs.
+// Modes: 0 = automatic for both tiles, 7 / 8 = forced for both, 1 = automatic for the halo
+// tile only (persistent tile at 256 rows), 2 = automatic for the persistent tile only.
+// Default 8: C3 runs its batch as two concurrent half-batch streams, which already fill the CUs a
+// short last round leaves idle, and there the 256-row tiles' better bytes-per-MFMA wins -- C3
+// end to end 6.00 (8) vs 6.11 (0) / 6.03 (1) / 6.07 (2) ms; with ONE stream the automatic
+// choice wins, 6.62 vs 6.78 ms (profiles/r04/ab_c3_rb224.txt).
 int g_pp_rb = -1;
+bool rb_mode_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 7 || v == 8; }
 int pp_rb_mode() {
   if (g_pp_rb < 0) {
     const char* e = getenv("PIPNET_PP_RB");
-    const int v = e ? atoi(e) : 0;
-    g_pp_rb = (v == 7 || v == 8) ? v : 0;
+    const int v = e ? atoi(e) : 8;
+    g_pp_rb = rb_mode_ok(v) ? v : 8;
   }
   return g_pp_rb;
 }
-int pick_rb(int M, int nt) {
-  const int forced = pp_rb_mode();
-  if (forced == 7 || forced == 8) return forced;
+int pick_rb(int M, int nt, bool halo) {
+  const int mode = pp_rb_mode();
+  if (mode == 7 || mode == 8) return mode;
+  if ((mode == 1 && !halo) || (mode == 2 && halo)) return 8;
   const int64_t ncu = num_cus();
   auto cost = [&](int rb) {
     const int64_t tiles = (int64_t)((M + 32 * rb - 1) / (32 * rb)) * nt;
@@ -172,7 +180,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   }
   if (v == 9) {                                  // persistent 256 x 256 ping-pong (1x1, N % 256 == 0)
     p.nt = p.N / 256;
-    const int rb = pick_rb(p.M, p.nt);
+    const int rb = pick_rb(p.M, p.nt, false);
     p.mt = (p.M + 32 * rb - 1) / (32 * rb);
     p.group_m = choose_group_m(p.K);
     const int ntiles = p.mt * p.nt;
@@ -198,7 +206,7 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   if (v == 8) {                                  // ping-pong with the LDS input halo, 256 x 64 NB
     const int nb = halo_nb(p.N);
     p.nt = (p.N + 64 * nb - 1) / (64 * nb);
-    const int rb = nb == 4 ? pick_rb(p.M, p.nt) : 8;
+    const int rb = nb == 4 ? pick_rb(p.M, p.nt, true) : 8;
     p.mt = (p.M + 32 * rb - 1) / (32 * rb);
     p.group_m = choose_group_m(p.K);
     const dim3 grid(p.mt * p.nt);
@@ -434,7 +442,7 @@ extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int C
 }
 
 extern "C" int pipnet_conv_bf16_rb(int mode) {
-  if (mode == 0 || mode == 7 || mode == 8) g_pp_rb = mode;
+  if (rb_mode_ok(mode)) g_pp_rb = mode;
   else if (mode != -1) return -PIPNET_ERR_ARG;
   return pp_rb_mode();
 }

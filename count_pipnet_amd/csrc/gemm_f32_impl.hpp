@@ -56,14 +56,15 @@ struct GemmParams {
   int rows_per_scale;
 };
 
-// Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 8
+// Lab instrumentation (ABL & 8, tools/gemm_stamps.py): thread 0 of each workgroup records 16
 // int64: start, first K-tile landed, main loop done, epilogue done (s_memtime), HW_ID,
-// XCC_ID, s_memrealtime at start and end.
+// XCC_ID, s_memrealtime at start and end; 8.. = epilogue sub-phases (vector epilogue: per
+// 32-row slab, accumulators re-laid through LDS / its stores issued).
 template <int ABL>
 PIPNET_DEV void lab_stamp(const GemmParams& p, int slot) {
   if constexpr ((ABL & 8) != 0) {
     if (threadIdx.x == 0) {
-      long long* s = p.stamps + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 8;
+      long long* s = p.stamps + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * 16;
       s[slot] = (long long)__builtin_amdgcn_s_memtime();
       if (slot == 0) {
         s[4] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -316,7 +317,7 @@ PIPNET_DEV void st4_c(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinte
 // whole main loop on the K=96 GEMMs.  All residual float4 loads of a lane are issued
 // before the first store (one latency, not sixteen).  Needs N % 4 == 0, ldc / ldr % 4 ==
 // 0, 16-B aligned C / R, and 32 KiB of the kernel's LDS (free after the main loop).
-template <int EPI, int TM, class AccT>
+template <int EPI, int TM, class AccT, int ABL = 0>
 PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, int m0, int n0, int wm, int wn,
                              int lane, int wid) {
   constexpr bool HAS_R = EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_MUL || EPI == PIPNET_EPI_BIAS_RESID_RELU ||
@@ -344,6 +345,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
     __syncthreads();
     slab_write(wt, acc, i, lane);
     __syncthreads();
+    lab_stamp<ABL>(p, 8 + 2 * i);
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int row = it * 4 + (lane >> 4);
@@ -353,6 +355,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
       const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
       if (m < p.M && nok) st4_c(p.C + (int64_t)m * p.ldc + n, x);
     }
+    lab_stamp<ABL>(p, 9 + 2 * i);
   }
 }
 
@@ -427,15 +430,27 @@ PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int
 
 // JL = how many of the wave's two 32-column blocks take part (2 everywhere except NPAD
 // waves whose blocks lie past N); a compile-time count, so the MFMA stream stays branch-free.
-template <int TM, int JL = 2>
+// AG ("GELU on A-load", pipnet_linear_agelu_f32): the A operand is gelu_erf of the stored
+// values, applied to each fragment in registers right before its MFMAs -- gelu_pk16 of the same
+// fp32 value the fused Linear1 epilogue would have computed, so the products are bitwise those
+// of the GELU-epilogue path (the GELU VALU work moves from a Linear1 epilogue, where it stalls
+// the MFMA pipe, into the Linear2 main loop, where it issues between MFMAs).
+PIPNET_DEV f32x4 gelu4(f32x4 x) {
+  const f32x2 lo = gelu_pk16(f32x2{x[0], x[1]}), hi = gelu_pk16(f32x2{x[2], x[3]});
+  return f32x4{lo[0], lo[1], hi[0], hi[1]};
+}
+template <int TM, int JL = 2, bool AG = false>
 PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
+  f32x4 a[2];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) a[i] = AG ? gelu4(f.a[i]) : f.a[i];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < JL; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][e], f.b[j][e], acc[i][j], 0, 0, 0);
 }
 
 // v_mfma_f32_16x16x4_f32 operands (cdna_hip_programming.md section 3: lane l supplies
@@ -502,10 +517,11 @@ PIPNET_DEV void wait_dma_barrier() {
 // workgroups land on different SIMDs (a relabelling: every output is computed identically).
 // SH = MFMA shape: 0 = v_mfma_f32_32x32x2_f32, 1 = v_mfma_f32_16x16x4_f32 (same tile, LDS image,
 // DMA and fragment bytes; a different k order inside each K-tile, so a different rounding).
-template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD>
+template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD, bool AG = false>
 PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
   using G = Geo<BK, TM>;
   static_assert(SH == 0 || BK == 32, "16x16x4 fragments: BK 32 (the swizzle is conflict-free there)");
+  static_assert(!AG || (SH == 0 && ALOAD == ALOAD_DENSE), "GELU on A-load: dense A, 32x32x2 MFMAs");
   // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
   const int nk_all = p.K / BK;
   const int kt_begin = (int)((int64_t)nk_all * blockIdx.y / gridDim.y);
@@ -641,19 +657,19 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
       }
       if constexpr (G::NGROUPS == 4) {
         read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-        mfma_frag<TM, JL>(acc, fa);
+        mfma_frag<TM, JL, AG>(acc, fa);
         read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
-        mfma_frag<TM, JL>(acc, fb);
+        mfma_frag<TM, JL, AG>(acc, fb);
         read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
-        mfma_frag<TM, JL>(acc, fa);
+        mfma_frag<TM, JL, AG>(acc, fa);
       } else {
         read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
-        mfma_frag<TM, JL>(acc, fa);
+        mfma_frag<TM, JL, AG>(acc, fa);
       }
       const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
       if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
       if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
-      mfma_frag<TM, JL>(acc, fb);
+      mfma_frag<TM, JL, AG>(acc, fb);
       cur = nxt;
     }
     }
@@ -675,7 +691,7 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
     return;
   }
   if (p.vec_epi)
-    epilogue_vec<EPI, TM>(p, acc, smem, m0, n0, wm, wn, lane, wid);
+    epilogue_vec<EPI, TM, AccT, ABL>(p, acc, smem, m0, n0, wm, wn, lane, wid);
   else if constexpr (SH == 0)
     epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lr, lh);
   else
@@ -686,10 +702,10 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
   }
 }
 
-template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false>
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0, bool NPAD = false, bool AG = false>
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM>::TILE_FLOATS];
-  gemm_tn_body<0, BK, TM, EPI, ALOAD, NS, ABL, NPAD>(p, smem);
+  gemm_tn_body<0, BK, TM, EPI, ALOAD, NS, ABL, NPAD, AG>(p, smem);
 }
 
 // the same tile on v_mfma_f32_16x16x4_f32

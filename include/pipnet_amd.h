@@ -66,11 +66,31 @@ int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* 
                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                       int M, int N, int K, int epilogue, void* stream);
 
+/* Dense fp32 linear with GELU applied to the A operand as it is loaded:
+ *   C[M,N] (ldc) = epi( gelu_erf(A[M,K]) (lda) * W[N,K]^T ),  epi in {NONE, BIAS, RESID}
+ * The CNBlock MLP (torchvision block.3 Linear, block.4 GELU, block.5 Linear + layer_scale +
+ * residual) runs as pipnet_linear_f32(EPI_BIAS) + this call (EPI_RESID): the GELU moves from
+ * Linear1's epilogue into Linear2's main loop, bitwise the same result.  K % 32 == 0, N % 4 == 0,
+ * lda / ldc / ldr % 4 == 0, 16-B aligned operands, and a shape served by the 32-deep tiles
+ * (K > 96): PIPNET_ERR_ARG otherwise (use the EPI_BIAS_GELU epilogue then). */
+int pipnet_linear_agelu_f32(const float* A, int64_t lda, const float* W, const float* bias,
+                            const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
+                            int M, int N, int K, int epilogue, void* stream);
+
 /* Persistent 128x128 fp32 GEMM tile for the 128-row / 2-stage shapes with N % 128 == 0
  * (stage-3/4 CNBlock Linears): mode 1 on, 0 off, -1 query only.  Returns the mode in force
  * (initially PIPNET_GEMM_PERSIST from the environment, else the build default) or a
  * negative status.  Not thread-safe against concurrent launches (process-wide A/B switch). */
 int pipnet_gemm_persist(int mode);
+
+/* 3-workgroups-per-CU fp32 GEMM tile (128 rows, 16-deep K-tiles, 2 LDS stages) for the short-K
+ * wide-N GEMMs (N % 128 == 0, N >= 1024, 256 <= K <= 512: the stage-3 CNBlock Linear1 + GELU):
+ * mode 1 on, 0 off, -1 query.  Returns the mode in force (initially PIPNET_GEMM_BK16X3 from the
+ * environment, else the build default) or a negative status.  Its 32x32x2 MFMAs pair k with
+ * k + 8 instead of k + 16 (a different fp32 summation order, exact-fp32 products either way);
+ * the choice depends on the layer's N and K only, so results stay batch-invariant.
+ * Process-wide switch, not thread-safe against concurrent launches. */
+int pipnet_gemm_bk16x3(int mode);
 
 /* Streaming persistent 128x128 fp32 GEMM tile (stage-3/4 CNBlock Linears: N % 128 == 0,
  * K % 32 == 0, K >= 256, >= 4 tiles per CU): two workgroups per CU walk their tiles as one
@@ -469,9 +489,10 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
                               float* d_logits, void* stream);
 
 /* Row blocks of the 256-wide bf16 ping-pong tiles (the LDS-halo 3x3 tile and the persistent 1x1
- * tile): mode 7 forces 224-row tiles, 8 forces 256-row tiles, 0 restores the automatic choice
- * (the form with fewer tile rounds per CU, conv_bf16.hip pick_rb; initially PIPNET_PP_RB from the
- * environment), -1 queries.  Returns the mode in force or a negative status.  Both forms compute
+ * tile): mode 7 forces 224-row tiles, 8 forces 256-row tiles (the default: C3's two concurrent
+ * streams fill short last rounds already), 0 = the automatic choice (the form with fewer tile
+ * rounds per CU, conv_bf16.hip pick_rb: faster for one-stream callers), 1 / 2 = automatic for the
+ * halo / the persistent tile only, -1 queries; initially PIPNET_PP_RB from the environment.  Returns the mode in force or a negative status.  Both forms compute
  * every output element with the same MFMA chain over the same K order: bitwise equal outputs.
  * Process-wide A/B switch, not thread-safe against concurrent launches. */
 int pipnet_conv_bf16_rb(int mode);

@@ -467,8 +467,8 @@ def test_pp_tiles_224_rows_bitwise(gpu, kind, m_or_b, cin, cout, epi):
     launch give bit for bit the 256-row forms' outputs (same MFMA chain and K order per element;
     the automatic choice between them depends on M, so batch invariance rests on this); ragged M,
     every epilogue, the one-A-piece waves' counted waits and the halo image borders."""
-    g = torch.Generator().manual_seed(m_or_b + cin)
     outs = {}
+    prev = K.conv_bf16_rb(-1)
     try:
         for rb in (8, 7):
             assert K.conv_bf16_rb(rb) == rb
@@ -497,7 +497,7 @@ def test_pp_tiles_224_rows_bitwise(gpu, kind, m_or_b, cin, cout, epi):
             outs[rb] = (out,)
         torch.cuda.synchronize()
     finally:
-        K.conv_bf16_rb(0)
+        K.conv_bf16_rb(prev)
     for a, b_ in zip(outs[8], outs[7]):
         assert torch.equal(a, b_)
-    assert K.conv_bf16_rb(-1) == 0
+    assert K.conv_bf16_rb(-1) == prev

@@ -436,3 +436,55 @@ def test_gemm_stream_bitwise(gpu, m, n, k, epi):
     elif epi == "bias":
         ref = ref + b.double()
     assert (outs[1][:m].double() - ref).abs().max().item() < 1e-3
+
+
+@pytest.mark.parametrize("m,c,hid", [(2000, 384, 1536), (1000, 768, 3072), (1234, 96, 384), (777, 192, 768)])
+def test_linear_agelu_bitwise_equals_gelu_epilogue(gpu, m, c, hid):
+    """pipnet_linear_agelu_f32 (GELU applied to Linear2's A fragments in registers) gives bit for
+    bit the EPI_BIAS_GELU Linear1 + plain Linear2 path of the CNBlock MLP (same gelu_pk16 of the
+    same fp32 values, same MFMA chain): 128-row tiles (stage 3/4 widths), 64-row tiles (N <= 384)
+    and the padded-column (N % 128 != 0) instantiation, the residual epilogue in place."""
+    from count_pipnet_amd import kernels as K, _lib
+    g = torch.Generator().manual_seed(m + c)
+    t = torch.randn(m, c, generator=g).to(gpu)
+    w1 = (torch.randn(hid, c, generator=g) / c ** 0.5).to(gpu)
+    b1 = torch.randn(hid, generator=g).to(gpu)
+    w2 = (torch.randn(c, hid, generator=g) / hid ** 0.5).to(gpu)
+    b2 = torch.randn(c, generator=g).to(gpu)
+    ls = torch.rand(c, generator=g).to(gpu)
+    x = torch.randn(m, c, generator=g).to(gpu)
+    u_gelu = K.linear(t, w1, b1, _lib.EPI_BIAS_GELU)
+    y_ref = x.clone()
+    K.linear(u_gelu, w2, b2, _lib.EPI_RESID, scale=ls, r=y_ref, out=y_ref)
+    u_pre = K.linear(t, w1, b1, _lib.EPI_BIAS)
+    y = x.clone()
+    K.linear_agelu(u_pre, w2, b2, _lib.EPI_RESID, scale=ls, r=y, out=y)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_ref)
+    # and against fp64 torch (exact GELU) at fp32 tolerance
+    ref = x.double() + ls.double() * (torch.nn.functional.gelu(t.double() @ w1.double().t() + b1.double())
+                                      @ w2.double().t() + b2.double())
+    assert (y.double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+
+
+def test_defer_gelu_network_bitwise(gpu):
+    """C2's CNBlocks with the GELU on Linear2's A-load (the default) and in Linear1's epilogue give
+    bitwise the same network outputs."""
+    from count_pipnet_amd import convnext_features as CF
+    from count_pipnet_amd.synthetic import synth_images
+    from golden_util import load_golden
+    from model_util import build_model
+    meta, _ = load_golden("c2_pipnet_convnext26")
+    net = build_model(meta).to(gpu).eval()
+    xs = synth_images(3, 224, seed=9).to(gpu)
+    outs = {}
+    prev = CF.DEFER_GELU
+    try:
+        for flag in (False, True):
+            CF.DEFER_GELU = flag
+            with torch.no_grad():
+                outs[flag] = [o.clone() for o in net(xs, inference=True)]
+    finally:
+        CF.DEFER_GELU = prev
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)

@@ -1,10 +1,12 @@
-"""Interleaved A/B of a module-level switch of the HIP path on one BASELINE config, in one process
-(cdna_hip_programming.md rule 24): rounds of (off, on) timings of net(xs, inference=True).
+"""Interleaved A/B of a switch of the HIP path on one BASELINE config, in one process
+(cdna_hip_programming.md rule 24): rounds of per-arm timings of net(xs, inference=True).
 
     python tools/ab_toggle.py <module>.<FLAG> <config> [--rounds 5] [--steps 10]
-e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3
-A library switch function instead of a module flag: fn:<module>.<func>:<off arg>:<on arg>,
-e.g. fn:count_pipnet_amd.kernels.conv_bf16_rb:8:0 (256-row tiles vs the automatic choice)."""
+e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3  (arms False, True)
+A library switch function instead of a module flag: fn:<module>.<func>:<arg>:<arg>[:<arg>...],
+one arm per argument, e.g. fn:count_pipnet_amd.kernels.conv_bf16_rb:8:0:1 (256-row tiles, the
+automatic choice, automatic for the halo tile only).  Prints one JSON line per arm and whether
+every arm's outputs are bitwise equal to the first arm's."""
 import argparse
 import importlib
 import json
@@ -28,15 +30,17 @@ def main():
     ap.add_argument("--stream-split", type=int, default=0, help="0 = the model's default")
     a = ap.parse_args()
     if a.flag.startswith("fn:"):
-        _, path, off, on = a.flag.split(":")
-        modname, fname = path.rsplit(".", 1)
+        parts = a.flag.split(":")
+        modname, fname = parts[1].rsplit(".", 1)
         fn = getattr(importlib.import_module(modname), fname)
+        arms = [int(v) for v in parts[2:]]
 
         def switch(val):
-            fn(int(on if val else off))
+            fn(val)
     else:
         modname, attr = a.flag.rsplit(".", 1)
         mod = importlib.import_module(modname)
+        arms = [False, True]
 
         def switch(val):
             setattr(mod, attr, val)
@@ -47,11 +51,11 @@ def main():
     if a.stream_split:
         from count_pipnet_amd.pipnet import set_stream_split
         set_stream_split(net, a.stream_split)
-    res = {False: [], True: []}
+    res = {v: [] for v in arms}
     outs = {}
     with torch.no_grad():
         for r in range(a.rounds):
-            for val in (False, True):
+            for val in arms:
                 switch(val)
                 for _ in range(2):
                     o = net(xs, inference=True)
@@ -65,13 +69,14 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res[val].append(e0.elapsed_time(e1) / a.steps)
-    same = all(torch.equal(x, y) for x, y in zip(outs[False], outs[True]))
-    for val in (False, True):
+    switch(arms[0])
+    for val in arms:
         ms = sorted(res[val])
         print(json.dumps({"flag": a.flag, "value": val, "config": a.config, "stream_split": a.stream_split or "default",
-                          "ms_median": ms[len(ms) // 2],
-                          "ms_min": ms[0], "img_s_median": cfg["batch"] / ms[len(ms) // 2] * 1e3}))
-    print(json.dumps({"outputs_bitwise_equal": same}))
+                          "ms_median": ms[len(ms) // 2], "ms_min": ms[0],
+                          "img_s_median": cfg["batch"] / ms[len(ms) // 2] * 1e3,
+                          "bitwise_equal_to_first_arm": all(torch.equal(x, y) for x, y in
+                                                            zip(outs[arms[0]], outs[val]))}))
 
 
 if __name__ == "__main__":

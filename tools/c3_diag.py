@@ -74,7 +74,7 @@ def main():
         flops = 2.0 * m * n * k
         tiles256 = -(-m // 256) * -(-n // 256)
         line = f"{name:8s} M={m:6d} N={n:5d} K={k:5d} tiles256={tiles256:5d} waves={tiles256 / 256:5.2f}"
-        K.conv_bf16_rb(0)
+        K.conv_bf16_rb(8)
         for key, v in res.items():
             ms = sorted(v)[len(v) // 2]
             line += f"  {key}: {flops / ms / 1e9:7.1f} TF ({ms * 1e3:7.1f} us)"

@@ -61,13 +61,13 @@ def main():
         s = torch.randn(n, device=dev, generator=g)
         R = torch.randn(m, n, device=dev, generator=g)
         C = torch.empty(m, n, device=dev)
-        st = torch.zeros(nwg * 8, dtype=torch.int64, device=dev)
+        st = torch.zeros(nwg * 16, dtype=torch.int64, device=dev)
         lib.lab_set_stamps(st.data_ptr())
         for _ in range(4):
             assert lib.lab_linear(v, 8, A.data_ptr(), k, W.data_ptr(), b.data_ptr(), s.data_ptr(), R.data_ptr(), n,
                                   C.data_ptr(), n, m, n, k, epi, stream) == 0
         torch.cuda.synchronize()
-        a = st.view(nwg, 8).cpu().numpy()
+        a = st.view(nwg, 16).cpu().numpy()
         lib.lab_set_stamps(None)
         pro, main_, epi_ = a[:, 1] - a[:, 0], a[:, 2] - a[:, 1], a[:, 3] - a[:, 2]
         rt0, rt1 = a[:, 6], a[:, 7]
@@ -84,6 +84,17 @@ def main():
         print(f"   cycles median: prologue {np.median(pro):.0f}  main {np.median(main_):.0f} "
               f"({np.median(main_) / nk:.0f}/K-tile)  epilogue {np.median(epi_):.0f} | "
               f"p90 prologue {np.percentile(pro, 90):.0f} epi {np.percentile(epi_, 90):.0f}", flush=True)
+        if (a[:, 8] > 0).all():          # vector epilogue sub-phases (wave 0's view), cycles
+            ph = [a[:, 8] - a[:, 2], a[:, 9] - a[:, 8]]
+            names = ["relayout0", "math+stores0"]
+            if (a[:, 10] > 0).all():
+                ph += [a[:, 10] - a[:, 9], a[:, 11] - a[:, 10], a[:, 3] - a[:, 11]]
+                names += ["relayout1", "math+stores1", "to end"]
+            else:
+                ph += [a[:, 3] - a[:, 9]]
+                names += ["to end"]
+            print("   epilogue median cycles: " + "  ".join(f"{nm} {np.median(v):.0f}" for nm, v in zip(names, ph)),
+                  flush=True)
         share = (pro.sum(), main_.sum(), epi_.sum())
         tot = sum(share)
         print(f"   wg-time share: prologue {share[0] / tot:.3f} main {share[1] / tot:.3f} epilogue {share[2] / tot:.3f}"
