@@ -14,3 +14,5 @@ timeout -k 10 300 python tools/ab_toggle.py count_pipnet_amd.convnext_features.D
 grep "^{" $O/ab_c2_defer_gelu.log
 timeout -k 10 600 python bench.py > $O/bench.log 2>&1; step bench $?
 tail -1 $O/bench.log | cut -c1-600
+LAB_ROUNDS=5 timeout -k 10 400 python tools/mlp_lab.py > $O/mlp_lab.log 2>&1; step mlplab $?
+grep -v "^\[\|amdgpu.ids" $O/mlp_lab.log | tail -12
