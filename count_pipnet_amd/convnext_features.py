@@ -236,9 +236,10 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
 
 FUSED_MLP = True      # tools / A-B runs may switch the fused narrow-stage MLP off
 # CNBlock GELU applied on Linear2's A-load (pipnet_linear_agelu_f32) rather than in Linear1's
-# epilogue; False = the fused-epilogue form (bitwise the same outputs; tools/ab_toggle.py
-# count_pipnet_amd.convnext_features.DEFER_GELU c2)
-DEFER_GELU = True
+# epilogue: bitwise the same outputs, but C2 22.06 -> 24.31 ms per step (tools/ab_toggle.py
+# count_pipnet_amd.convnext_features.DEFER_GELU c2, profiles/r04/ab_c2_defer_gelu.txt): the
+# packed GELU VALU between Linear2's MFMAs stalls them more than Linear1's epilogue did.  Off.
+DEFER_GELU = False
 # The fused MLP parallelises over pixels only (16 per wave): on small feature maps (C1's 64^2
 # inputs: 256 / 64 pixels per image) the unfused GEMMs, which also spread the hidden dimension
 # over workgroups, are faster.  The choice depends on the layer's C and h*w, never on the batch

@@ -180,6 +180,26 @@ PIPNET_DEV f32x2 gelu_pk(f32x2 x) {
 
 constexpr int EPI_LAB_GELU_PK = 100;     // tuning lab only: BIAS_GELU through gelu_pk
 constexpr int EPI_LAB_GELU_PK16 = 101;   // tuning lab only: BIAS_GELU through gelu_pk16
+constexpr int EPI_LAB_GELU_SC16 = 102;   // tuning lab only: gelu_pk16's math on unpacked scalars
+constexpr int EPI_LAB_GELU_FAST = 103;   // tuning lab only: gelu_fast (scalar erfc fit, 1 rcp + 1 exp)
+
+// gelu_pk16's A&S 7.1.28 arithmetic with scalar (unpacked) fp32 instructions: packed VALU beside
+// another wave's MFMAs costs more than two scalar ops (MI355X_MICROARCH.md cycle constants).
+// Not bitwise gelu_pk16 (the packed and scalar fmas round alike, but hipcc may contract differently).
+PIPNET_DEV float gelu_sc16(float x) {
+  const float hx = x * 0.5f, ahx = fabsf(hx);
+  float p = fmaf(ahx, 0.00034451040f, 0.0015645004f);
+  p = fmaf(ahx, p, 0.00060805720f);
+  p = fmaf(ahx, p, 0.026221010f);
+  p = fmaf(ahx, p, 0.084564020f);
+  p = fmaf(ahx, p, 0.099734694f);
+  p = fmaf(ahx, p, 1.0f);
+  p = p * p;
+  p = p * p;
+  p = p * p;
+  p = p * p;
+  return fmaf(-ahx, __builtin_amdgcn_rcpf(p), hx + ahx);
+}
 
 using Acc = f32x16[2][2];
 
@@ -276,6 +296,11 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
     x = x + bn;
     const f32x2 lo = gelu_pk16(f32x2{x[0], x[1]}), hi = gelu_pk16(f32x2{x[2], x[3]});
     x = f32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+  if (EPI == EPI_LAB_GELU_SC16 || EPI == EPI_LAB_GELU_FAST) {
+    x = x + bn;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) x[e] = EPI == EPI_LAB_GELU_SC16 ? gelu_sc16(x[e]) : gelu_fast(x[e]);
   }
   if (EPI == EPI_LAB_GELU_PK || EPI == EPI_LAB_GELU_PK16) {
     x = x + bn;

@@ -203,15 +203,12 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
       if (ci + 1 < G::NCHH) stage(ci + 1);
       const float* buf = smem + (ci % 3) * G::STAGE_F + part * G::CHUNK_F;
       const float* prev = smem + ((ci + 2) % 3) * G::STAGE_F + part * G::CHUNK_F;   // chunk ci-1
-      if (!late) {
-        if (ci < G::NCHH) {
-          f32x4 h[PX][NHB];
-          gemm1_gelu(buf, ci, h);
-          gemm2(buf, h);
-        }
-      } else {
-        if (ci > 0) gemm2(prev, hk);
-        if (ci < G::NCHH) gemm1_gelu(buf, ci, hk);
+      // one GEMM1 + GELU site for both halves; GEMM2 of the late half before it (chunk ci-1),
+      // of the early half after it (chunk ci)
+      if (late && ci > 0) gemm2(prev, hk);
+      if (ci < G::NCHH) {
+        gemm1_gelu(buf, ci, hk);
+        if (!late) gemm2(buf, hk);
       }
     }
   } else

@@ -3,6 +3,7 @@
 
     python tools/ab_toggle.py <module>.<FLAG> <config> [--rounds 5] [--steps 10]
 e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3  (arms False, True)
+Stream splits as arms: streams:1:2:3.
 A library switch function instead of a module flag: fn:<module>.<func>:<arg>:<arg>[:<arg>...],
 one arm per argument, e.g. fn:count_pipnet_amd.kernels.conv_bf16_rb:8:0:1 (256-row tiles, the
 automatic choice, automatic for the halo tile only).  Prints one JSON line per arm and whether
@@ -29,7 +30,14 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--stream-split", type=int, default=0, help="0 = the model's default")
     a = ap.parse_args()
-    if a.flag.startswith("fn:"):
+    net_holder = {}
+    if a.flag.startswith("streams:"):            # arms = stream splits of the model itself
+        arms = [int(v) for v in a.flag.split(":")[1:]]
+
+        def switch(val):
+            from count_pipnet_amd.pipnet import set_stream_split
+            set_stream_split(net_holder["net"], val)
+    elif a.flag.startswith("fn:"):
         parts = a.flag.split(":")
         modname, fname = parts[1].rsplit(".", 1)
         fn = getattr(importlib.import_module(modname), fname)
@@ -47,6 +55,7 @@ def main():
     dev = torch.device("cuda:0")
     cfg = bc.CONFIGS[a.config]
     net = bc.make(cfg, dev)
+    net_holder["net"] = net
     xs = synth_images(cfg["batch"], cfg["size"], seed=1).to(dev)
     if a.stream_split:
         from count_pipnet_amd.pipnet import set_stream_split

@@ -27,6 +27,10 @@ static void launch(GemmParams& p, int epi, hipStream_t s) {
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_PK, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
   else if (epi == EPI_LAB_GELU_PK16)
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_PK16, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+  else if (epi == EPI_LAB_GELU_SC16)
+    hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_SC16, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
+  else if (epi == EPI_LAB_GELU_FAST)
+    hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, EPI_LAB_GELU_FAST, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
   else if (epi == PIPNET_EPI_BIAS)
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_BIAS, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
   else if (epi == PIPNET_EPI_RESID)
