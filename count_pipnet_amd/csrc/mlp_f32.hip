@@ -64,7 +64,8 @@ struct MlpGeo {
 // the barrier -- so the two waves of a SIMD reach their GELU (VALU, MFMA pipe idle) at different
 // times instead of together after every chunk barrier.  Three LDS stages (W2 of chunk ci-1 stays
 // valid through period ci), one extra barrier period at the end.  Every wave sums the same terms
-// in the same order: bitwise the unstaggered kernel's output.
+// in the same order: bitwise the unstaggered kernel's output.  Lab only (tools/mlp_lab.hip): no
+// faster on any C2 / C5 shape, so the product launches ST = false (profiles/r04/mlp_stagger_lab.txt).
 template <int C, int HC, int NW, int PX, int HS = 1, bool ST = false>
 __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
