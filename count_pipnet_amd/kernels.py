@@ -344,6 +344,23 @@ def conv_bf16_rb(mode: int = -1) -> int:
     return r
 
 
+PP_DS_DEFAULT = 0          # mirrors PIPNET_PP_DS_DEFAULT (csrc/conv_bf16.hip)
+
+
+def conv_bf16_direct_epi(mode: int = -1) -> int:
+    """The library's epilogue switch of the persistent 1x1 bf16 tile (include/pipnet_amd.h
+    pipnet_conv_bf16_direct_epi): 1 = direct from registers, 0 = through LDS, -1 queries."""
+    r = _lib.load().pipnet_conv_bf16_direct_epi(mode)
+    if r < 0:
+        _lib.check(-r, f"pipnet_conv_bf16_direct_epi({mode})")
+    return r
+
+
+def _pp_ds() -> str:
+    ds = conv_bf16_direct_epi(-1) if torch.cuda.is_available() else PP_DS_DEFAULT
+    return "true" if ds else "false"
+
+
 def bf16_pp_rb(m: int, nt: int, halo: bool = False) -> int:
     """Row blocks per wave group the library picks for a halo / persistent tile grid of ``nt``
     256-wide column tiles (mirrors pick_rb in csrc/conv_bf16.hip): 7 (224-row tiles) when that
@@ -369,7 +386,7 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
-        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}>"
+        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}, {_pp_ds()}>"
     if t == 8:
         nb = 4 if n >= 256 else (2 if n >= 128 else 1)
         rb = bf16_pp_rb(m, -(-n // (64 * nb)), halo=True) if nb == 4 else 8
@@ -486,7 +503,8 @@ def conv1x1_bf16_dual(x: Tensor, w_packed: Tensor, bias: Tensor, n1: int, n2: in
     y1 = torch.empty((b, h, w, n1), device=x.device, dtype=torch.bfloat16)
     y2 = torch.empty((b, h, w, n2), device=x.device, dtype=torch.bfloat16)
     m = b * h * w
-    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}>", 2.0 * m * (n1 + n2) * cin,
+    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}, {_pp_ds()}>",
+            2.0 * m * (n1 + n2) * cin,
             lambda: _lib.call("pipnet_conv1x1_bf16_dual", x.data_ptr(), m, cin, w_packed.data_ptr(), bias.data_ptr(),
                               n1, y1.data_ptr(), n2, y2.data_ptr(), _stream(x)))
     return y1, y2
@@ -555,16 +573,17 @@ MLP_HS2_MAX_HW = 256    # C = 192 on maps of <= 16 x 16: hidden split over two w
 
 
 def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20, hw: int = 0) -> str:
-    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32)."""
+    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32; the last
+    template argument is the lab-only staggered form, never launched by the product)."""
     if c == 192 and 0 < hw <= MLP_HS2_MAX_HW:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 2, false>"
     if c == 96:
         nw = 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
-        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
+        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1, false>"
     if m >= 32768:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 1>"
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 1, false>"
     nw = 4 if m >= 8192 else 2 if m >= 4096 else 1
-    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
+    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1, false>"
 
 
 def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor,

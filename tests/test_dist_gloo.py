@@ -119,6 +119,7 @@ def _group_worker(rank, world, port, q):
         ok = (pooled.shape[0] == 4 and torch.allclose(pooled, r_pooled, atol=1e-6)
               and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5) and wrapped.world == 4 and wrapped.rank == rank % 4)
         q.put((rank, bool(ok)))
+        dist.barrier()          # rank 0 hosts the store: no rank leaves while another group still uses it
     finally:
         dist.destroy_process_group()
 

@@ -595,6 +595,127 @@ __global__ __launch_bounds__(256, 1) void lab_q4_kernel(ConvParams p) {
 }
 }  // namespace pipnet_bf16
 
+namespace pipnet_bf16 {
+// Lab-only: lab_q4_kernel with the accumulators pinned to AGPRs by inline-asm MFMAs ("+a"
+// operands): hipcc's own allocation of the 256 accumulators split them over VGPRs and AGPRs
+// (361 v_accvgpr moves + scratch in the loop, profiles/r02/bf16_lab.txt).  Same k order and
+// MFMA as pp: bitwise equal outputs.  ABL: 2 = no epilogue.
+PIPNET_DEV void mfma_acc(f32x4v& c, const bf16x8v& a, const bf16x8v& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+template <int ABL>
+__global__ __launch_bounds__(256, 1) void lab_q4a_kernel(ConvParams p) {
+  using namespace pp;
+  constexpr int NS = 4, NW = 4, TMF = 8, TNF = 8;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[NS * STAGE_BYTES];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  int m0, n0;
+  tile_coords(p, BM, BN, m0, n0);
+  const int nk = p.K / BK;
+  const int drow = lane >> 2;
+  const int dchunk = 8 * ((lane & 3) ^ g(drow));
+  const bf16* asrc[4];
+  const bf16* wsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 16 * (wid + NW * i) + drow;
+    asrc[i] = p.A + (int64_t)min(m0 + row, p.M - 1) * p.lda + dchunk;
+    wsrc[i] = p.W + (int64_t)min(n0 + row, p.N - 1) * p.K + dchunk;
+  }
+  auto stage = [&](int kt) {
+    unsigned char* base = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(asrc[i] + kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + (wid + NW * i) * 1024), 16,
+                                       0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(wsrc[i] + kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + BM * ROWB + (wid + NW * i) * 1024),
+                                       16, 0, 0);
+  };
+  const int fr = lane & 15;
+  const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
+  bf16x8v fa[2][TMF], fb[2][TNF];
+  auto read = [&](int kt, bf16x8v (&a)[TMF], bf16x8v (&b)[TNF]) {
+    const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+#pragma unroll
+    for (int n = 0; n < TNF; ++n)
+      b[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 128 + n * 16) * ROWB + fofs);
+#pragma unroll
+    for (int r = 0; r < TMF; ++r) a[r] = *reinterpret_cast<const bf16x8v*>(st + (wr * 128 + r * 16) * ROWB + fofs);
+  };
+  f32x4v acc[TMF][TNF];
+#pragma unroll
+  for (int r = 0; r < TMF; ++r)
+#pragma unroll
+    for (int n = 0; n < TNF; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < 3 && t < nk; ++t) stage(t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  read(0, fa[0], fb[0]);
+  auto step = [&](int kt, auto sc) {
+    constexpr int S = decltype(sc)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + 3 < nk) stage(kt + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = 0; r < TMF / 2; ++r)
+#pragma unroll
+      for (int n = 0; n < TNF; ++n) mfma_acc(acc[r][n], fa[S][r], fb[S][n]);
+    __builtin_amdgcn_s_setprio(0);
+    const int younger = (kt + 2 < nk) + (kt + 3 < nk);
+    if (younger == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    pp_barrier();
+    if (kt + 1 < nk) read(kt + 1, fa[S ^ 1], fb[S ^ 1]);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int r = TMF / 2; r < TMF; ++r)
+#pragma unroll
+      for (int n = 0; n < TNF; ++n) mfma_acc(acc[r][n], fa[S][r], fb[S][n]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, IntC<0>{});
+    step(kt + 1, IntC<1>{});
+  }
+  if (kt < nk) step(kt, IntC<0>{});
+  // the MFMAs are opaque to the hazard recognizer: pad before the accumulators are read
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
+  if constexpr ((ABL & 2) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < TMF; ++r)
+#pragma unroll
+      for (int n = 0; n < TNF; ++n)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t += acc[r][n][i];
+    reinterpret_cast<float*>(p.C)[(int64_t)blockIdx.x * 256 + tid] = t;
+    return;
+  }
+#pragma unroll
+  for (int r = 0; r < TMF; ++r)
+#pragma unroll
+    for (int n = 0; n < TNF; ++n)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wr * 128 + r * 16 + 4 * (lane >> 4) + i;
+        const int nn = n0 + wc * 128 + n * 16 + (lane & 15);
+        if (m < p.M && nn < p.N) p.C[(int64_t)m * p.ldc + nn] = (bf16)acc[r][n][i];
+      }
+}
+}  // namespace pipnet_bf16
+
 namespace {
 int group_for(int K, double budget) {
   const double panel = 128.0 * K * 2.0;
@@ -633,6 +754,8 @@ extern "C" int lab_pp(int abl, const void* A, const void* W, void* C, int M, int
     case 512: hipLaunchKernelGGL((lab_prs2_kernel<0>), grid, dim3(512), 0, s, p); break;
     case 1024: hipLaunchKernelGGL((lab_q4_kernel<0>), grid, dim3(256), 0, s, p); break;
     case 1026: hipLaunchKernelGGL((lab_q4_kernel<2>), grid, dim3(256), 0, s, p); break;
+    case 1040: hipLaunchKernelGGL((lab_q4a_kernel<0>), grid, dim3(256), 0, s, p); break;
+    case 1042: hipLaunchKernelGGL((lab_q4a_kernel<2>), grid, dim3(256), 0, s, p); break;
     case 514: hipLaunchKernelGGL((lab_prs2_kernel<2>), grid, dim3(512), 0, s, p); break;
     LAB_CP(0, 0, 0) LAB_CP(1, 1, 1) LAB_CP(2, 2, 2) LAB_CP(3, 16, 16) LAB_CP(4, 17, 17) LAB_CP(5, 2, 0)
     LAB_CP(6, 0, 2) LAB_CP(7, 3, 3) LAB_CP(8, 16, 0) LAB_CP(9, 0, 16)

@@ -3,6 +3,7 @@ interleaved rounds in one process (cdna_hip_programming.md rule 24), uniform [-1
 
     python tools/bf16_lab.py                 # builds tools/libbf16_lab.so if missing
     LAB_ABL=0,1,2,4 LAB_SHAPES=sq8192,l4ds python tools/bf16_lab.py
+    LAB_ABL=0,1040,-1 ...   (1040 / 1042: the four-wave tile with AGPR accumulators; -1: hipBLASLt)
 """
 import ctypes
 import os
@@ -53,7 +54,7 @@ def main():
         c = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
         res = {}
         # correctness: the full-line kernel accumulates in the same k order as the 32-deep one
-        for alt in (32, 256, 512, 1024):
+        for alt in (32, 256, 512, 1024, 1040):
             if alt not in abls or 0 not in abls:
                 continue
             c2 = torch.empty_like(c)
@@ -68,6 +69,9 @@ def main():
             for abl in abls:
                 for bud in budgets:
                     def run():
+                        if abl < 0:                                  # -1: hipBLASLt (torch matmul)
+                            torch.matmul(a, w.t(), out=c)
+                            return
                         st = lib.lab_pp(abl, a.data_ptr(), w.data_ptr(), c.data_ptr(), m, n, k, bud, stream)
                         assert st == 0, st
                     for _ in range(2):
