@@ -28,7 +28,6 @@ SIGNATURES = {
     "pipnet_gemm_persist": [I32],
     "pipnet_gemm_stream": [I32],
     "pipnet_conv_bf16_rb": [I32],
-    "pipnet_conv_bf16_direct_epi": [I32],
     "pipnet_gemm_bk16x3": [I32],
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_agelu_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],

@@ -126,20 +126,6 @@ int pp_rb_mode() {
   }
   return g_pp_rb;
 }
-// Epilogue of the persistent 1x1 tile: 1 = direct (swapped MFMA operands + permlane16_swap, no
-// LDS round trip; gemm_bf16_impl.hpp conv_bf16_ppp_kernel DS), 0 = through LDS.  Bitwise the
-// same outputs.  pipnet_conv_bf16_direct_epi or PIPNET_PP_DS=0/1 in the environment switch it.
-#ifndef PIPNET_PP_DS_DEFAULT
-#define PIPNET_PP_DS_DEFAULT 0
-#endif
-int g_pp_ds = -1;
-int pp_ds_mode() {
-  if (g_pp_ds < 0) {
-    const char* e = getenv("PIPNET_PP_DS");
-    g_pp_ds = e ? (atoi(e) != 0) : PIPNET_PP_DS_DEFAULT;
-  }
-  return g_pp_ds;
-}
 int pick_rb(int M, int nt, bool halo) {
   const int mode = pp_rb_mode();
   if (mode == 7 || mode == 8) return mode;
@@ -199,13 +185,10 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     p.group_m = choose_group_m(p.K);
     const int ntiles = p.mt * p.nt;
     const dim3 grid(ntiles < num_cus() ? ntiles : num_cus());
-    const bool ds = pp_ds_mode() != 0;
 #define PIPNET_PPP(E)                                                                                  \
   case E:                                                                                               \
-    if (rb == 7 && ds) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 7, true>), grid, dim3(512), 0, s, p); \
-    else if (rb == 7) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 7, false>), grid, dim3(512), 0, s, p); \
-    else if (ds) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 8, true>), grid, dim3(512), 0, s, p);     \
-    else hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 8, false>), grid, dim3(512), 0, s, p);            \
+    if (rb == 7) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 7>), grid, dim3(512), 0, s, p);           \
+    else hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 8>), grid, dim3(512), 0, s, p);                   \
     break;
     switch (epi) {
       PIPNET_PPP(PIPNET_EPI_NONE)
@@ -462,12 +445,6 @@ extern "C" int pipnet_conv_bf16_rb(int mode) {
   if (rb_mode_ok(mode)) g_pp_rb = mode;
   else if (mode != -1) return -PIPNET_ERR_ARG;
   return pp_rb_mode();
-}
-
-extern "C" int pipnet_conv_bf16_direct_epi(int mode) {
-  if (mode == 0 || mode == 1) g_pp_ds = mode;
-  else if (mode != -1) return -PIPNET_ERR_ARG;
-  return pp_ds_mode();
 }
 
 extern "C" int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias,

@@ -789,14 +789,7 @@ PIPNET_DEV void tile_coords_id(const ConvParams& p, int id, int bm, int bn, int&
 // pick_rb: fewer idle CUs in the last round; bitwise the same outputs).  With RB = 7 the A tile
 // is 14 DMA pieces of 16 rows: waves 0-5 issue two per K-tile, waves 6-7 one (na), and every
 // counted wait uses the wave's own count.
-// DS = direct epilogue: the MFMAs take the weight fragment as their FIRST operand, so each
-// lane's accumulator holds 4 consecutive channels of one pixel (D^T: row = channel, column =
-// pixel) instead of 4 pixels of one channel; one v_permlane16_swap per fp32 pair of adjacent
-// 16-channel blocks then gives every lane 8 consecutive channels, finished and stored as 16 B
-// straight from registers -- no LDS round trip (16 ds_write_b32 + 2 ds_read_b128 + two
-// lgkmcnt(0) drains per 16 rows per lane).  The products and their k order are those of the
-// other operand order: bitwise the same outputs.
-template <int EPI, int RB = 8, bool DS = false>
+template <int EPI, int RB = 8>
 __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) {
   using namespace pp;
   constexpr int DB = 2, NS = 4;
@@ -872,11 +865,6 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     else pp_wait_vm<4 + X>();
   };
 
-  auto mm = [](const bf16x8v& a, const bf16x8v& b, const f32x4v& c) {
-    if constexpr (DS) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, 0, 0, 0);
-    else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  };
-
   int m0, n0;
   int id = blockIdx.x;
   setup(id, m0, n0);
@@ -903,7 +891,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[r][n] = mm(fa[r], fb[n], acc[r][n]);
+        for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
       if (STEADY || kt + DB + 1 < nk) stage_a(kt + DB + 1);
@@ -916,7 +904,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       for (int r = 0; r < RB - 4; ++r)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[4 + r][n] = mm(fa[r], fb[n], acc[4 + r][n]);
+          acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
     };
@@ -931,7 +919,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[r][n] = mm(fa[r], fb[n], acc[r][n]);
+        for (int n = 0; n < 4; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
       stage_a(DB + 1);
@@ -943,7 +931,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       for (int r = 0; r < RB - 4; ++r)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[4 + r][n] = mm(fa[r], fb[n], acc[4 + r][n]);
+          acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
       pp_barrier();
       kt = 1;
@@ -966,80 +954,13 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     // loads and output stores are non-temporal: C3 21.6k -> 22.1k img/s median over five
     // interleaved runs (profiles/r03/ppp_nt_epilogue_ab.log) -- fewer caches lines for this
     // stream of read-once / written-once tiles; bits unchanged ----
+    float* wt = reinterpret_cast<float*>(smem + ppp::OFF_EPI) + wid * 16 * 64;
+    const int c8 = lane & 7;
+    const int n = cn0 + wc * 64 + 8 * c8;
     // EPI_DUAL_BIAS_RELU: a whole 256-wide tile lies on one side of nsplit (both % 256 == 0)
     const bool second = EPI == PIPNET_EPI_DUAL_BIAS_RELU && cn0 >= p.nsplit;
     bf16* const cout = second ? p.C2 : p.C;
     const int64_t ldo = second ? p.ldc2 : p.ldc;
-    if constexpr (DS) {
-      // lane: pixel row fr of each 16-row block; after the swap of blocks (2j, 2j+1), channels
-      // 32 j + dsc .. +7 of the wave's 64, dsc = 0 / 16 / 8 / 24 for lane rows q = 0..3
-      const int q = lane >> 4;
-      const int dsc = 8 * ((q >> 1) | ((q & 1) << 1));
-      f32x4v bj[2][2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = cn0 + wc * 64 + 32 * j + dsc;
-        bj[j][0] = bj[j][1] = f32x4v{0.f, 0.f, 0.f, 0.f};
-        if (EPI != PIPNET_EPI_NONE && p.bias) {
-          bj[j][0] = *reinterpret_cast<const f32x4v*>(p.bias + n);
-          bj[j][1] = *reinterpret_cast<const f32x4v*>(p.bias + n + 4);
-        }
-      }
-      bf16x8v rr[16];
-      if (HAS_R) {
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int m = min(cm0 + wr * 16 * RB + r * 16 + fr, p.M - 1);
-            rr[2 * r + j] = __builtin_bit_cast(bf16x8v, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
-                                p.R + (int64_t)m * p.ldr + cn0 + wc * 64 + 32 * j + dsc)));
-          }
-      }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int m = min(cm0 + wr * 16 * RB + r * 16 + fr, p.M - 1);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x4v x0 = acc[r][2 * j], x1 = acc[r][2 * j + 1];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const auto sw = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, x0[e]),
-                                                             __builtin_bit_cast(unsigned, x1[e]), false, false);
-            x0[e] = __builtin_bit_cast(float, (unsigned)sw[0]);
-            x1[e] = __builtin_bit_cast(float, (unsigned)sw[1]);
-          }
-          x0 += bj[j][0];
-          x1 += bj[j][1];
-          if (HAS_R) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              x0[e] += (float)rr[2 * r + j][e];
-              x1[e] += (float)rr[2 * r + j][4 + e];
-            }
-          }
-          if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU || second) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              x0[e] = fmaxf(x0[e], 0.f);
-              x1[e] = fmaxf(x1[e], 0.f);
-            }
-          }
-          bf16x8v o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o[e] = (bf16)x0[e];
-            o[4 + e] = (bf16)x1[e];
-          }
-          const int n = cn0 + wc * 64 + 32 * j + dsc;
-          const int no = second ? n - p.nsplit : n;
-          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(cout + (int64_t)m * ldo + no));
-        }
-      }
-    } else {
-    float* wt = reinterpret_cast<float*>(smem + ppp::OFF_EPI) + wid * 16 * 64;
-    const int c8 = lane & 7;
-    const int n = cn0 + wc * 64 + 8 * c8;
     const int no = second ? n - p.nsplit : n;
     f32x4v b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0;
     if (EPI != PIPNET_EPI_NONE && p.bias) {
@@ -1098,7 +1019,6 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(cout + (int64_t)m * ldo + no));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
     }
     if (!more) break;
     // next tile's A(0) / B(0): younger are A1 B1 A2 (6) and this epilogue's stores (and, with a

@@ -344,23 +344,6 @@ def conv_bf16_rb(mode: int = -1) -> int:
     return r
 
 
-PP_DS_DEFAULT = 0          # mirrors PIPNET_PP_DS_DEFAULT (csrc/conv_bf16.hip)
-
-
-def conv_bf16_direct_epi(mode: int = -1) -> int:
-    """The library's epilogue switch of the persistent 1x1 bf16 tile (include/pipnet_amd.h
-    pipnet_conv_bf16_direct_epi): 1 = direct from registers, 0 = through LDS, -1 queries."""
-    r = _lib.load().pipnet_conv_bf16_direct_epi(mode)
-    if r < 0:
-        _lib.check(-r, f"pipnet_conv_bf16_direct_epi({mode})")
-    return r
-
-
-def _pp_ds() -> str:
-    ds = conv_bf16_direct_epi(-1) if torch.cuda.is_available() else PP_DS_DEFAULT
-    return "true" if ds else "false"
-
-
 def bf16_pp_rb(m: int, nt: int, halo: bool = False) -> int:
     """Row blocks per wave group the library picks for a halo / persistent tile grid of ``nt``
     256-wide column tiles (mirrors pick_rb in csrc/conv_bf16.hip): 7 (224-row tiles) when that
@@ -386,7 +369,7 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
-        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}, {_pp_ds()}>"
+        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}>"
     if t == 8:
         nb = 4 if n >= 256 else (2 if n >= 128 else 1)
         rb = bf16_pp_rb(m, -(-n // (64 * nb)), halo=True) if nb == 4 else 8
@@ -503,7 +486,7 @@ def conv1x1_bf16_dual(x: Tensor, w_packed: Tensor, bias: Tensor, n1: int, n2: in
     y1 = torch.empty((b, h, w, n1), device=x.device, dtype=torch.bfloat16)
     y2 = torch.empty((b, h, w, n2), device=x.device, dtype=torch.bfloat16)
     m = b * h * w
-    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}, {_pp_ds()}>",
+    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}>",
             2.0 * m * (n1 + n2) * cin,
             lambda: _lib.call("pipnet_conv1x1_bf16_dual", x.data_ptr(), m, cin, w_packed.data_ptr(), bias.data_ptr(),
                               n1, y1.data_ptr(), n2, y2.data_ptr(), _stream(x)))

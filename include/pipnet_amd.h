@@ -497,13 +497,6 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
  * Process-wide A/B switch, not thread-safe against concurrent launches. */
 int pipnet_conv_bf16_rb(int mode);
 
-/* Epilogue form of the persistent 1x1 bf16 tile: 1 = direct from registers (swapped MFMA
- * operands, one v_permlane16_swap per pair of 16-channel blocks, 16-B stores), 0 = re-laid
- * through LDS; -1 queries.  Returns the mode in force or -PIPNET_ERR_ARG.  Bitwise equal outputs
- * (same products, same k order).  Process-wide A/B switch, not thread-safe against concurrent
- * launches. */
-int pipnet_conv_bf16_direct_epi(int mode);
-
 /* fp64-accumulated product for inference-time weight folds (csrc/fold_f64.hip):
  *   C[M,N] (ldc) = RNE_f32( sum_k double(A[m,k]) * double(B[k,n]) ), A [M,K] (lda) and B [K,N]
  *   (ldb) row-major fp32, products and sums in fp64 on v_mfma_f64_16x16x4_f64, any sizes.

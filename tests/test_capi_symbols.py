@@ -102,7 +102,7 @@ def test_roofline_kernel_names_exist_in_library():
                  (192, 1024)]:                                 # fused narrow-stage MLP (csrc/mlp_f32.hip)
         assert K.cnblock_mlp_kernel_name(c, m) in out, (c, m)
     assert K.cnblock_mlp_kernel_name(192, 16384, hw=256) in out          # hidden split (C5 stage 2)
-    assert "pipnet_bf16::conv_bf16_ppp_kernel<12, 8, false>" in out                  # dual 1x1 (downsample + conv1)
+    assert "pipnet_bf16::conv_bf16_ppp_kernel<12, 8>" in out                  # dual 1x1 (downsample + conv1)
     assert "pipnet_bf16::stem_pool_bf16_kernel" in out                     # fused stem + max-pool
     for m, c in ((401408, 64), (100352, 128)):                               # small-N halo tile (11)
         assert K.bf16_conv_kernel_name(m, c, _lib.EPI_BIAS_RELU, 2, kv=9 * c, halo64_ok=True) in out

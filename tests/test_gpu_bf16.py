@@ -501,46 +501,3 @@ def test_pp_tiles_224_rows_bitwise(gpu, kind, m_or_b, cin, cout, epi):
     for a, b_ in zip(outs[8], outs[7]):
         assert torch.equal(a, b_)
     assert K.conv_bf16_rb(-1) == prev
-
-
-@pytest.mark.parametrize("kind,m,cin,cout,epi", [
-    ("1x1", 2352, 256, 256, _lib.EPI_BIAS_RELU),
-    ("1x1", 50176, 1024, 256, _lib.EPI_BIAS_RELU),
-    ("1x1", 5000, 256, 1024, _lib.EPI_BIAS_RESID_RELU),
-    ("1x1", 777, 512, 512, _lib.EPI_BIAS),
-    ("1x1", 300, 128, 256, _lib.EPI_NONE),
-    ("dual", 4704, 512, (1024, 256), None)])
-def test_ppp_direct_epilogue_bitwise(gpu, kind, m, cin, cout, epi):
-    """The persistent 1x1 tile's direct epilogue (swapped MFMA operands + permlane16_swap, 16-B
-    stores from registers) writes bit for bit what the LDS re-layout epilogue writes: every
-    epilogue, ragged M (clamped duplicate rows), 224- and 256-row tiles, the dual launch."""
-    prev_ds, prev_rb = K.conv_bf16_direct_epi(-1), K.conv_bf16_rb(-1)
-    gg = torch.Generator().manual_seed(11)
-    if kind == "dual":
-        n1, n2 = cout
-        x = torch.randn(1, m, 1, cin, generator=gg).to(torch.bfloat16).to(gpu)
-        wp = K.pack_conv_weight_bf16((torch.randn(n1 + n2, 1, 1, cin, generator=gg) * 0.05).to(gpu))
-        b = torch.randn(n1 + n2, generator=gg).to(gpu)
-        run = lambda: K.conv1x1_bf16_dual(x, wp, b, n1, n2)          # noqa: E731
-    else:
-        x = torch.randn(1, m, 1, cin, generator=gg).to(torch.bfloat16).to(gpu)
-        wp = K.pack_conv_weight_bf16((torch.randn(cout, 1, 1, cin, generator=gg) / cin ** 0.5).to(gpu))
-        r = torch.randn(1, m, 1, cout, generator=gg).to(torch.bfloat16).to(gpu)
-        b = torch.randn(cout, generator=gg).to(gpu)
-        run = lambda: (K.conv2d_nhwc_bf16(x, wp, 1, 1, None if epi == _lib.EPI_NONE else b, 1, 0, epi,   # noqa: E731
-                                          r if epi == _lib.EPI_BIAS_RESID_RELU else None),)
-    outs = {}
-    try:
-        for rb in (8, 7):
-            K.conv_bf16_rb(rb)
-            for ds in (0, 1):
-                assert K.conv_bf16_direct_epi(ds) == ds
-                outs[(rb, ds)] = [t.clone() for t in run()]
-        torch.cuda.synchronize()
-    finally:
-        K.conv_bf16_direct_epi(prev_ds)
-        K.conv_bf16_rb(prev_rb)
-    for key, o in outs.items():
-        for a, b_ in zip(outs[(8, 0)], o):
-            assert torch.equal(a, b_), key
-    assert K.conv_bf16_direct_epi(-1) == prev_ds

@@ -43,12 +43,10 @@ def main():
     ap.add_argument("--tiles", default="9,5")
     ap.add_argument("--rb", default="8", help="row-block forms of tile 9 to time (7 = 224-row tiles)")
     ap.add_argument("--only", default=None)
-    ap.add_argument("--ds", default="0", help="epilogue forms of tile 9 to time (1 = direct from registers)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
     tiles = [int(t) for t in a.tiles.split(",")]
-    kd = K.conv_bf16_direct_epi(-1)
     for name, m, n, k in SHAPES:
         if a.only and name not in a.only.split(","):
             continue
@@ -58,16 +56,13 @@ def main():
         wb = w.to(torch.bfloat16)
         b = torch.randn(n, device=dev, generator=g)
         x2 = x.view(m, k)
-        def conv(t, rb, ds):
+        def conv(t, rb):
             K.conv_bf16_rb(rb)
-            K.conv_bf16_direct_epi(ds)
             return K.conv2d_nhwc_bf16(x, wp, 1, 1, b, 1, 0, _lib.EPI_BIAS_RELU, None, tile=t)
         fns = {}
         for t in tiles:
             for rb in ([int(v) for v in a.rb.split(",")] if t == 9 else [8]):
-                for ds in ([int(v) for v in a.ds.split(",")] if t == 9 else [0]):
-                    key = f"t{t}" + (f"r{rb}" if t == 9 else "") + (f"d{ds}" if t == 9 and "," in a.ds else "")
-                    fns[key] = (lambda t=t, rb=rb, ds=ds: conv(t, rb, ds))
+                fns[f"t{t}" + (f"r{rb}" if t == 9 else "")] = (lambda t=t, rb=rb: conv(t, rb))
         fns["lib"] = lambda: torch.nn.functional.linear(x2, wb)
         for f in fns.values():
             f(), f()
@@ -80,7 +75,6 @@ def main():
         tiles256 = -(-m // 256) * -(-n // 256)
         line = f"{name:8s} M={m:6d} N={n:5d} K={k:5d} tiles256={tiles256:5d} waves={tiles256 / 256:5.2f}"
         K.conv_bf16_rb(8)
-        K.conv_bf16_direct_epi(kd)
         for key, v in res.items():
             ms = sorted(v)[len(v) // 2]
             line += f"  {key}: {flops / ms / 1e9:7.1f} TF ({ms * 1e3:7.1f} us)"
