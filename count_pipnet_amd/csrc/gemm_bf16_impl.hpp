@@ -507,16 +507,22 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
     s1 = *reinterpret_cast<const f32x4v*>(p.scale + n + 4);
   }
   // residual rows of both halves requested up front: one HBM latency per tile, not two
+  // running row pointers (+8 rows per step): no per-access 64-bit multiply (ppp epilogue note)
+  const int mrow0 = mw + (lane >> 3);
   bf16x8v rrs[2][8];
   if (HAS_R) {
+    const bf16* rp = p.R + (int64_t)mrow0 * p.ldr + n;
+    const bf16* const rlast = p.R + (int64_t)(p.M - 1) * p.ldr + n;
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
       for (int it = 0; it < 2 * (half ? RB - 4 : 4); ++it) {
-        const int m = min(mw + half * 64 + it * 8 + (lane >> 3), p.M - 1);
-        if (nok) rrs[half][it] = *reinterpret_cast<const bf16x8v*>(p.R + (int64_t)m * p.ldr + n);
+        const bf16* src = mrow0 + half * 64 + it * 8 < p.M ? rp : rlast;
+        if (nok) rrs[half][it] = *reinterpret_cast<const bf16x8v*>(src);
+        rp += 8 * p.ldr;
       }
   }
+  bf16* op = p.C + (int64_t)mrow0 * p.ldc + n;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int nr = half ? RB - 4 : 4;            // row blocks of this half (compile-time after unrolling)
@@ -561,7 +567,8 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
         o[e] = (bf16)x0[e];
         o[4 + e] = (bf16)x1[e];
       }
-      if (m < p.M && nok) *reinterpret_cast<bf16x8v*>(p.C + (int64_t)m * p.ldc + n) = o;
+      if (m < p.M && nok) *reinterpret_cast<bf16x8v*>(op) = o;
+      op += 8 * p.ldc;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // reads done before the next half's writes
   }
@@ -967,15 +974,24 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       b0 = *reinterpret_cast<const f32x4v*>(p.bias + n);
       b1 = *reinterpret_cast<const f32x4v*>(p.bias + n + 4);
     }
+    // Row addresses: lane row (lane >> 3) of 8-row step q is mq = mrow0 + 8 q, clamped to M - 1.
+    // One 64-bit row product per tile and a running pointer (+8 rows per step) with a select
+    // for the clamped rows -- a per-store (int64) m * ld costs three quarter-rate integer
+    // multiplies, which made up a third of this VALU-bound epilogue's cycles.
+    const int mrow0 = cm0 + wr * 16 * RB + (lane >> 3);
     bf16x8v rr[16];
     if (HAS_R) {
+      const bf16* rp = p.R + (int64_t)mrow0 * p.ldr + n;
+      const bf16* const rlast = p.R + (int64_t)(p.M - 1) * p.ldr + n;
 #pragma unroll
       for (int q = 0; q < 2 * RB; ++q) {
-        const int m = min(cm0 + wr * 16 * RB + q * 8 + (lane >> 3), p.M - 1);
-        rr[q] = __builtin_bit_cast(bf16x8v, __builtin_nontemporal_load(
-                    reinterpret_cast<const u32x4*>(p.R + (int64_t)m * p.ldr + n)));   // read once
+        const bf16* src = mrow0 + 8 * q < p.M ? rp : rlast;
+        rr[q] = __builtin_bit_cast(bf16x8v, __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src)));  // read once
+        rp += 8 * p.ldr;
       }
     }
+    bf16* op = cout + (int64_t)mrow0 * ldo + no;
+    bf16* const olast = cout + (int64_t)(p.M - 1) * ldo + no;
     const int fq = lane >> 4;
 #pragma unroll
     for (int r = 0; r < RB; ++r) {
@@ -1015,8 +1031,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
           o[e] = (bf16)x0[e];
           o[4 + e] = (bf16)x1[e];
         }
-        const int m = min(cm0 + wr * 16 * RB + r * 16 + row, p.M - 1);
-        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(cout + (int64_t)m * ldo + no));
+        bf16* dst = mrow0 + 16 * r + 8 * it < p.M ? op : olast;     // row = it * 8 + (lane >> 3)
+        __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(dst));
+        op += 8 * ldo;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }

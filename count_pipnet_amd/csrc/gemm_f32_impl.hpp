@@ -355,16 +355,23 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
   if (EPI != PIPNET_EPI_NONE && EPI != PIPNET_EPI_MUL && EPI != PIPNET_EPI_GELU_BWD && p.bias && nok)
     bn = ld4(p.bias + n);   // (incl. lab GELU)
   if ((EPI == PIPNET_EPI_RESID || EPI == PIPNET_EPI_RESID_ROWSCALE) && p.scale && nok) sn = ld4(p.scale + n);
+  // Row addresses as running pointers (+4 rows per step; the residual's clamped rows by a
+  // select): a per-access (int64) m * ld is three quarter-rate integer multiplies per store.
+  const int mrow0 = m0 + wm * 32 * TM + (lane >> 4);
   f32x4 r[TM][8];
   if (HAS_R) {
+    const float* rp = p.R + (int64_t)mrow0 * p.ldr + n;
+    const float* const rlast = p.R + (int64_t)(p.M - 1) * p.ldr + n;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int it = 0; it < 8; ++it) {
-        const int m = min(m0 + wm * 32 * TM + i * 32 + it * 4 + (lane >> 4), p.M - 1);
-        r[i][it] = nok ? ld4(p.R + (int64_t)m * p.ldr + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* src = mrow0 + i * 32 + it * 4 < p.M ? rp : rlast;
+        r[i][it] = nok ? ld4(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rp += 4 * p.ldr;
       }
   }
+  float* op = p.C + (int64_t)mrow0 * p.ldc + n;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     __syncthreads();
@@ -378,7 +385,8 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
       float rs = 1.f;
       if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
       const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
-      if (m < p.M && nok) st4_c(p.C + (int64_t)m * p.ldc + n, x);
+      if (m < p.M && nok) st4_c(op, x);
+      op += 4 * p.ldc;
     }
     lab_stamp<ABL>(p, 9 + 2 * i);
   }

@@ -99,6 +99,24 @@ def main():
         tot = sum(share)
         print(f"   wg-time share: prologue {share[0] / tot:.3f} main {share[1] / tot:.3f} epilogue {share[2] / tot:.3f}"
               f" | resident WGs/CU avg {occ:.2f} over the span", flush=True)
+        # epilogue coincidence: per CU, how much of its workgroups' epilogue time overlaps another
+        # resident workgroup's epilogue (both slots off the MFMA pipe), memtime -> realtime per WG
+        scale = (rt1 - rt0) / np.maximum(a[:, 3] - a[:, 0], 1)
+        e0 = rt0 + (a[:, 2] - a[:, 0]) * scale
+        e1 = rt1
+        both = tot_e = 0.0
+        for c in np.unique(cu):
+            idx = np.nonzero(cu == c)[0]
+            ev = sorted([(e0[i], 1) for i in idx] + [(e1[i], -1) for i in idx])
+            depth, last = 0, None
+            for t, d in ev:
+                if last is not None and depth >= 2:
+                    both += t - last
+                depth += d
+                last = t
+            tot_e += (e1[idx] - e0[idx]).sum()
+        print(f"   epilogue coincidence: {2 * both / max(tot_e, 1):.3f} of epilogue time overlaps another epilogue on the CU "
+              f"(random phases at this share: ~{share[2] / tot:.3f})", flush=True)
         # tail: fraction of span after the first WG slot goes permanently idle
         order = np.sort(rt1)
         print(f"   tail: last 5% of WGs finish over {(order[-1] - order[int(0.95 * nwg)]) / 100:.1f}us, "
