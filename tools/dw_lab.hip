@@ -21,6 +21,11 @@ extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, c
   // v8-v10: narrower column tiles for small maps (a row tile of G * TX pixels against W = 32 / 16)
   V(8, 96, 4, 1, 1, 8) V(8, 192, 4, 1, 1, 16) V(9, 96, 4, 2, 1, 8) V(9, 192, 4, 2, 1, 16)
   V(10, 96, 2, 2, 1, 8) V(10, 192, 2, 2, 1, 16)
+  // v40-v43 (round 4): taller tiles now that each weight row is loaded once per workgroup
+  V(40, 96, 7, 2, 1, 8) V(40, 192, 7, 2, 1, 16) V(40, 384, 7, 2, 1, 32) V(40, 768, 7, 2, 1, 64)
+  V(41, 96, 7, 3, 1, 8) V(41, 192, 7, 3, 1, 16) V(41, 384, 7, 3, 1, 32) V(41, 768, 7, 3, 1, 64)
+  V(42, 96, 4, 2, 1, 8) V(42, 192, 4, 2, 1, 16) V(42, 384, 4, 2, 1, 32) V(42, 768, 4, 2, 1, 64)
+  V(43, 96, 4, 4, 1, 8) V(43, 192, 4, 4, 1, 16) V(43, 384, 4, 4, 1, 32) V(43, 768, 4, 4, 1, 64)
   R(1, 96, 4, 4, 2, 16) R(2, 96, 2, 4, 3, 16) R(3, 96, 4, 8, 1, 16) R(4, 96, 3, 4, 2, 16)
   R(1, 192, 4, 2, 2, 16) R(2, 192, 2, 2, 3, 16) R(3, 192, 4, 4, 1, 16) R(4, 192, 3, 2, 2, 16)
   R(1, 384, 4, 1, 2, 32) R(2, 384, 2, 1, 3, 32) R(3, 384, 4, 2, 1, 32) R(4, 384, 3, 1, 2, 32)
