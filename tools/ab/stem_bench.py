@@ -1,5 +1,6 @@
+import os
 import sys, torch
-sys.path.insert(0, '/root/repo')
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from count_pipnet_amd import kernels as K
 dev = torch.device('cuda:0')
 for (b, h) in [(64, 224), (16, 64), (64, 128)]:
