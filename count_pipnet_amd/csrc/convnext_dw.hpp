@@ -112,8 +112,17 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
   // per-element "load or zero" made hipcc branch around every load (exec-masked blocks) and
   // spend more issue slots on 64-bit address arithmetic than on the FMAs.
   const int voff0 = ((px0 - 3) * C + 4 * q) * 4;
+  // Weight row ky is loaded once, at input row ir = ky, and stays in registers for the TY
+  // output rows that use it (input rows ir = ky .. ky + TY - 1): with TY > 1 a per-use load
+  // re-read every weight TY times through the vector L1 -- the loads, not the FMAs, fill the
+  // L1 / TA path of this kernel.  Same FMA order: bitwise the per-use form's result.
+  f32x4 wrow[7][7];
 #pragma unroll
   for (int ir = 0; ir < TY + 6; ++ir) {
+    if (ir < 7) {
+#pragma unroll
+      for (int kx = 0; kx < 7; ++kx) wrow[ir][kx] = ld4(wp + (ir * 7 + kx) * C + 4 * q);
+    }
     const int iy = oy0 + ir - 3;
     if (iy < 0 || iy >= H) continue;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -128,7 +137,7 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
       if (ky < 0 || ky >= 7) continue;
 #pragma unroll
       for (int kx = 0; kx < 7; ++kx) {
-        const f32x4 wk = ld4(wp + (ky * 7 + kx) * C + 4 * q);
+        const f32x4 wk = wrow[ky][kx];
 #pragma unroll
         for (int px = 0; px < TX; ++px) acc[t][px] += v[px + kx] * wk;
       }

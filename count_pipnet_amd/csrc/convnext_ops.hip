@@ -205,7 +205,12 @@ extern "C" int pipnet_convnext_stem_f32(const float* x, int B, int H, int W, con
 // 59 -> 56 / 90 -> 85 us at the C2 stages).  Small maps take narrower column tiles (a row tile of
 // G * 7 pixels left 43 % of the lanes idle at W = 32 / 16): C5 stage 1 36.7 -> 26.2 us, stage 2
 // 18.2 -> 16.9 us; at C1's 16^2 / 8^2 maps (batch 16) the wide tile stays 2 % faster, hence the
-// lower bounds.  The choice depends on W only (per-pixel results stay batch-invariant).
+// lower bounds.  Round 4: with each weight row loaded once per workgroup (convnext_dw.hpp),
+// taller tiles (TY = 2-4 output rows) cut the vector-L1 traffic of the weights and the 7-row
+// input halo: C2 stages 68 -> 49 (96 @ 56^2), 34 -> 29 (192 @ 28^2), 56 -> 47 us (384 @ 27^2),
+// C5 stages 25 -> 17.5 (96 @ 32^2), 17 -> 12.4 us (192 @ 16^2); 768 @ 26^2 keeps TY = 1
+// (profiles/r04/dw_window_lab.txt).  Every tile sums the same 49 products in the same order:
+// bitwise equal outputs.  The choice depends on W only (per-pixel results stay batch-invariant).
 extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C, const float* w_packed,
                                      const float* bias, const float* ln_w, const float* ln_b, float* y,
                                      void* stream) {
@@ -218,12 +223,14 @@ extern "C" int pipnet_dwconv7_ln_f32(const float* x, int B, int H, int W, int C,
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
     case 96:
-      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 4, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 32) return pipnet_dw::launch_dw<96, 7, 2, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<96, 7, 1, 1, false, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192:
-      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 2, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16) return pipnet_dw::launch_dw<192, 7, 2, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<192, 7, 1, 1, false, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
-    case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, false, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 384: return pipnet_dw::launch_dw<384, 7, 3, 1, false, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     default: return PIPNET_ERR_ARG;
   }
@@ -240,12 +247,14 @@ extern "C" int pipnet_dwconv7_ln_s3(const float* x, int B, int H, int W, int C, 
   hipStream_t s = (hipStream_t)stream;
   switch (C) {
     case 96:
-      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 2, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16 && W <= 32) return pipnet_dw::launch_dw<96, 4, 4, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 32) return pipnet_dw::launch_dw<96, 7, 2, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<96, 7, 1, 1, true, 8>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 192:
-      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 8 && W <= 16) return pipnet_dw::launch_dw<192, 4, 2, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+      if (W > 16) return pipnet_dw::launch_dw<192, 7, 2, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
       return pipnet_dw::launch_dw<192, 7, 1, 1, true, 16>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
-    case 384: return pipnet_dw::launch_dw<384, 7, 1, 2, true, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
+    case 384: return pipnet_dw::launch_dw<384, 7, 3, 1, true, 32>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     case 768: return pipnet_dw::launch_dw<768, 13, 1, 1, true>(x, B, H, W, w_packed, bias, ln_w, ln_b, y, s);
     default: return PIPNET_ERR_ARG;
   }

@@ -357,7 +357,6 @@ def _optimizers_like_reference(net, meta, fwd_meta):
     return opt_net, opt_cls, sched_net, sched_cls
 
 
-@pytest.mark.parametrize("name", SUFFIX)
 def _resnet_first_grads_close(net, rec):
     """the AdamW trajectory bound is sign-like (it cannot see a right-sign gradient of
     the wrong magnitude), so pin the magnitude directly: the HIP gradients of iteration 0 -- the
@@ -388,6 +387,7 @@ def _resnet_first_grads_close(net, rec):
     assert checked > 0
 
 
+@pytest.mark.parametrize("name", SUFFIX)
 def test_suffix_training_matches_reference(gpu, name):
     meta, rec, fwd_meta = load_train_golden(name)
     net = build_model(fwd_meta).to(gpu).train()
