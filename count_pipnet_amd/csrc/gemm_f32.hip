@@ -113,6 +113,16 @@ bool gemm_bk16x3() {
   }
   return g_gemm_bk16x3 == 1;
 }
+// Output-tile store policy of the GEMMs launched through launch_gemm: 0 = non-temporal (default),
+// 1 = plain.  pipnet_gemm_plain_store or PIPNET_GEMM_PLAIN_STORE=1 switch it.
+int g_gemm_plain = -1;
+int gemm_plain_store() {
+  if (g_gemm_plain < 0) {
+    const char* e = getenv("PIPNET_GEMM_PLAIN_STORE");
+    g_gemm_plain = e ? (e[0] == '1') : 0;
+  }
+  return g_gemm_plain;
+}
 bool bk16x3_shape(const GemmParams& p) {
   return p.N % 128 == 0 && p.N >= 1024 && p.K % 16 == 0 && p.K >= 256 && p.K <= 512 && p.M > 64;
 }
@@ -125,6 +135,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
+  p.plain_store = gemm_plain_store();
   int v = gemm_variant(p.M, p.N, p.K, vec);
   if (v == 3 && epi != PIPNET_EPI_RESID_ROWSCALE && bk16x3_shape(p) && gemm_bk16x3()) v = 4;
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
@@ -205,6 +216,12 @@ extern "C" int pipnet_gemm_persist(int mode) {
   if (mode == 0 || mode == 1) g_gemm_persist = mode;
   else if (mode != -1) return PIPNET_ERR_ARG;
   return gemm_persist() ? 1 : 0;
+}
+
+extern "C" int pipnet_gemm_plain_store(int mode) {
+  if (mode == 0 || mode == 1) g_gemm_plain = mode;
+  else if (mode != -1) return PIPNET_ERR_ARG;
+  return gemm_plain_store();
 }
 
 extern "C" int pipnet_gemm_bk16x3(int mode) {

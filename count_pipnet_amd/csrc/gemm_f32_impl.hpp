@@ -48,6 +48,7 @@ struct GemmParams {
   int H, Wd, Cin, OH, OW, stride, KW, pad;
   int mt, nt, group_m;
   int vec_epi;     // 1: float4 epilogue through LDS (N, ldc, ldr % 4 == 0, C / R 16-B aligned)
+  int plain_store; // 1: output tiles stored with plain (cached) stores instead of non-temporal ones
   int stagger;     // lab: workgroups [stagger_lo, stagger_hi) sleep stagger x s_sleep(127) first
   int stagger_lo, stagger_hi;
   int64_t split_stride;   // split-K (gridDim.y > 1): slab y of C starts at C + y * split_stride
@@ -333,7 +334,12 @@ PIPNET_DEV f32x4 epi_math(f32x4 x, const f32x4& bn, const f32x4& sn, const f32x4
 // Output-tile store: non-temporal, so the streaming C tiles do not evict the A / W panels
 // other workgroups of the XCD still read (s384 fc1: 338 -> 184 MiB fetched per launch at
 // equal time, profiles/r02/gemm_raster_store_ab.txt).
-PIPNET_DEV void st4_c(float* p, f32x4 v) { __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p)); }
+// (GemmParams::plain_store: a cached store, for A/B of what the next kernel reads -- the consumer
+// of a non-temporally written tile fetches it from HBM rather than the Infinity Cache.)
+PIPNET_DEV void st4_c(float* p, f32x4 v, int plain = 0) {
+  if (plain) *reinterpret_cast<f32x4*>(p) = v;
+  else __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+}
 
 // Vectorised epilogue: each wave re-lays its accumulator tile through LDS (32 rows at a
 // time, 8 KiB per wave) so every global store / residual load is a float4 and one wave
@@ -385,7 +391,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
       float rs = 1.f;
       if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
       const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
-      if (m < p.M && nok) st4_c(op, x);
+      if (m < p.M && nok) st4_c(op, x, p.plain_store);
       op += 4 * p.ldc;
     }
     lab_stamp<ABL>(p, 9 + 2 * i);

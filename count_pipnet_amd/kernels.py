@@ -87,6 +87,12 @@ def gemm_stream(mode: int = -1) -> bool:
     return bool(r)
 
 
+def gemm_plain_store(mode: int = -1) -> int:
+    """The library's store-policy switch of the fp32 GEMM output tiles (include/pipnet_amd.h
+    pipnet_gemm_plain_store): 1 = plain cached stores, 0 = non-temporal (default), -1 queries."""
+    return _lib.load().pipnet_gemm_plain_store(mode)
+
+
 def gemm_bk16x3(mode: int = -1) -> bool:
     """The library's 3-workgroups-per-CU tile switch for short-K wide-N GEMMs (include/pipnet_amd.h
     pipnet_gemm_bk16x3): mode 1 / 0 sets it, -1 queries."""

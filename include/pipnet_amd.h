@@ -90,6 +90,10 @@ int pipnet_gemm_persist(int mode);
  * k + 8 instead of k + 16 (a different fp32 summation order, exact-fp32 products either way);
  * the choice depends on the layer's N and K only, so results stay batch-invariant.
  * Process-wide switch, not thread-safe against concurrent launches. */
+/* Store policy of the fp32 GEMM output tiles (pipnet_linear_f32 / conv paths): 1 = plain
+ * (cached) stores, 0 = non-temporal (default); -1 queries.  Same bits either way.  Process-wide A/B
+ * switch, not thread-safe against concurrent launches. */
+int pipnet_gemm_plain_store(int mode);
 int pipnet_gemm_bk16x3(int mode);
 
 /* Streaming persistent 128x128 fp32 GEMM tile (stage-3/4 CNBlock Linears: N % 128 == 0,
