@@ -30,6 +30,7 @@ SIGNATURES = {
     "pipnet_conv_bf16_rb": [I32],
     "pipnet_gemm_bk16x3": [I32],
     "pipnet_gemm_plain_store": [I32],
+    "pipnet_head_bf16_quads": [I32],
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_agelu_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],

@@ -8,6 +8,7 @@
 // One wave owns one patch: lane l holds channels l, l+64, ... so every HBM access is a
 // coalesced 256-B row segment, and the per-patch reductions are 64-lane butterflies.
 #include "common.hpp"
+#include <cstdlib>
 
 namespace {
 // Zero-fill by a kernel rather than a memset call: the launch is captured as an ordinary
@@ -182,6 +183,110 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const 
     else
       atomicAdd(dst, r);
   }
+}
+
+// Quad layout (round 4): lane l holds channels 4l + 256q .. +3 (8-B bf16 loads, 512 B contiguous
+// per wave instruction), so each 16-B fp32 proto store instruction writes 1 KiB contiguous -- 8
+// whole 128-B lines -- where the 8-channel layout above writes every line in two halves from
+// two instructions (proto is 2/3 of this kernel's bytes).  Same per-element exp / scale; the
+// per-lane partial sums of the softmax denominator group channels differently, so the last bits
+// of the denominator can differ from the 8-channel layout's.
+template <int NV, int MODE>
+__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const __bf16* __restrict__ feat, int HW,
+                                                                          int P, float* __restrict__ proto,
+                                                                          float* __restrict__ pooled) {
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  constexpr int NQ = 2 * NV;
+  __shared__ float red[HEAD_THREADS / 64][NV * 512];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = blockIdx.y;
+  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
+  float racc[NQ][4];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) racc[q][e] = 0.f;
+  constexpr int STEP = HEAD_THREADS / 64;
+  bf16x4_t xc[NQ], xn[NQ];
+  auto load_pix = [&](int pix, bf16x4_t (&x)[NQ]) {
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * lane + 256 * q;
+      if (c < P) x[q] = *reinterpret_cast<const bf16x4_t*>(feat + base + c);
+    }
+  };
+  if (wv < PIX_PER_BLOCK && pix0 + wv < HW) load_pix(pix0 + wv, xc);
+  for (int pi = wv; pi < PIX_PER_BLOCK; pi += STEP) {
+    const int pix = pix0 + pi;
+    if (pix >= HW) break;
+    if (pi + STEP < PIX_PER_BLOCK && pix + STEP < HW) load_pix(pix + STEP, xn);
+    const int64_t base = ((int64_t)b * HW + pix) * P;
+    float v[NQ][4];
+    float m = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const bool ok = 4 * lane + 256 * q < P;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[q][e] = ok ? (float)xc[q][e] : -INFINITY;
+        m = fmaxf(m, v[q][e]);
+      }
+    }
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[q][e] = 4 * lane + 256 * q < P ? expf(v[q][e] - m) : 0.f;
+        s += v[q][e];
+      }
+    const float inv = 1.0f / wave_sum(s);
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int c = 4 * lane + 256 * q;
+      if (c < P) {
+        f32x4 y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) y[e] = v[q][e] * inv;
+        __builtin_nontemporal_store(y, reinterpret_cast<f32x4*>(proto + base + c));   // write-once map
+#pragma unroll
+        for (int e = 0; e < 4; ++e) racc[q][e] = MODE == 0 ? fmaxf(racc[q][e], y[e]) : racc[q][e] + y[e];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) xc[q] = xn[q];
+  }
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) red[wv][4 * lane + 256 * q + e] = racc[q][e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
+    float r = red[0][c];
+#pragma unroll
+    for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
+    float* dst = pooled + (int64_t)b * P + c;
+    if (MODE == 0)
+      atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
+    else
+      atomicAdd(dst, r);
+  }
+}
+
+// bf16 head layout: 1 = quad layout (softmax_pool_bf16q_kernel), 0 = 8-channel layout;
+// pipnet_head_bf16_quads or PIPNET_HEAD_QUADS=0/1 switch it.
+#ifndef PIPNET_HEAD_QUADS_DEFAULT
+#define PIPNET_HEAD_QUADS_DEFAULT 0
+#endif
+static int g_head_quads = -1;
+static int head_quads() {
+  if (g_head_quads < 0) {
+    const char* e = getenv("PIPNET_HEAD_QUADS");
+    g_head_quads = e ? (e[0] == '1') : PIPNET_HEAD_QUADS_DEFAULT;
+  }
+  return g_head_quads;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -550,8 +655,13 @@ extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, 
   hipStream_t s = (hipStream_t)stream;
   if (!zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const bool quads = head_quads() && P % 4 == 0;
 #define SPV_CALL(N)                                                                                            \
-  if (pool_mode == 0)                                                                                          \
+  if (quads && pool_mode == 0)                                                                                 \
+    hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
+  else if (quads)                                                                                              \
+    hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
+  else if (pool_mode == 0)                                                                                     \
     hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
   else                                                                                                         \
     hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled);
@@ -565,6 +675,12 @@ extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, 
 #undef SPV_CALL
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
+}
+
+extern "C" int pipnet_head_bf16_quads(int mode) {
+  if (mode == 0 || mode == 1) g_head_quads = mode;
+  else if (mode != -1) return PIPNET_ERR_ARG;
+  return head_quads();
 }
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,

@@ -93,6 +93,12 @@ def gemm_plain_store(mode: int = -1) -> int:
     return _lib.load().pipnet_gemm_plain_store(mode)
 
 
+def head_bf16_quads(mode: int = -1) -> int:
+    """The library's layout switch of the bf16 prototype head (include/pipnet_amd.h
+    pipnet_head_bf16_quads): 1 = 4 channels per lane, 0 = 8 per lane, -1 queries."""
+    return _lib.load().pipnet_head_bf16_quads(mode)
+
+
 def gemm_bk16x3(mode: int = -1) -> bool:
     """The library's 3-workgroups-per-CU tile switch for short-K wide-N GEMMs (include/pipnet_amd.h
     pipnet_gemm_bk16x3): mode 1 / 0 sets it, -1 queries."""

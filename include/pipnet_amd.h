@@ -93,6 +93,11 @@ int pipnet_gemm_persist(int mode);
 /* Store policy of the fp32 GEMM output tiles (pipnet_linear_f32 / conv paths): 1 = plain
  * (cached) stores, 0 = non-temporal (default); -1 queries.  Same bits either way.  Process-wide A/B
  * switch, not thread-safe against concurrent launches. */
+/* Layout of the bf16 prototype head (pipnet_softmax_pool_bf16): 1 = 4 channels per lane (8-B
+ * loads, 16-B proto stores covering whole lines), 0 = 8 channels per lane (default); -1 queries.
+ * The softmax denominators' partial sums group differently (last-bit differences).  Process-wide
+ * A/B switch, not thread-safe against concurrent launches. */
+int pipnet_head_bf16_quads(int mode);
 int pipnet_gemm_plain_store(int mode);
 int pipnet_gemm_bk16x3(int mode);
 

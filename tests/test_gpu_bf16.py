@@ -501,3 +501,27 @@ def test_pp_tiles_224_rows_bitwise(gpu, kind, m_or_b, cin, cout, epi):
     for a, b_ in zip(outs[8], outs[7]):
         assert torch.equal(a, b_)
     assert K.conv_bf16_rb(-1) == prev
+
+
+@pytest.mark.parametrize("b,hw,p", [(3, 784, 2048), (2, 49, 512), (1, 37, 1000), (2, 10, 8)])
+def test_head_bf16_quad_layout(gpu, b, hw, p):
+    """The bf16 head's 4-channels-per-lane layout (whole-line proto stores) against the
+    8-channels-per-lane one and an fp32 torch softmax + max-pool of the same bf16 logits: only
+    the softmax denominators' partial-sum grouping differs (a few ulp)."""
+    x = (torch.randn(b, 1, hw, p, generator=torch.Generator().manual_seed(3)) * 3).to(torch.bfloat16).to(gpu)
+    prev = K.head_bf16_quads(-1)
+    outs = {}
+    try:
+        for q in (0, 1):
+            assert K.head_bf16_quads(q) == q
+            proto, pooled = K.softmax_pool_bf16(x, pool_mode=0)
+            outs[q] = (proto.clone(), pooled.clone())
+        torch.cuda.synchronize()
+    finally:
+        K.head_bf16_quads(prev)
+    ref = torch.softmax(x.float().view(b, hw, p), dim=-1)
+    for q, (proto, pooled) in outs.items():
+        torch.testing.assert_close(proto.view(b, hw, p), ref, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(pooled, ref.amax(dim=1), rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-6, atol=1e-9)
+    assert K.head_bf16_quads(-1) == prev
