@@ -11,9 +11,10 @@ Semantics versus the eager forward:
     output tensors (overwritten by the next replay -- clone them to keep them);
   * weights are read at replay time from the same addresses, so in-place updates of
     parameters (``eval_pipnet``'s classifier sparsification, pipnet/test.py:71-73) are seen;
-    repacked copies (depthwise taps, BN-folded ResNet convs, bf16 weights) are the ones
-    captured -- re-capture after ``load_state_dict`` or any weight change other than the
-    classification layer's;
+    repacked copies (depthwise taps, BN-folded ResNet convs, bf16 weights, the folded
+    BilinearIntermediate weights W E / V E) are the ones captured -- re-capture after
+    ``load_state_dict`` or any weight change other than the classification layer's (and call
+    ``invalidate_weight_caches(net)`` first when the change went through ``.data``);
   * the CountPIPNet Gumbel noise is drawn from a device-resident Philox key advanced on the
     stream by every replay (``pipnet_count_gumbel_devseed_f32``): fresh noise per call, as
     the reference draws (count_pipnet_utils.py:36-38);
