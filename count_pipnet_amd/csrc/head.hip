@@ -275,10 +275,11 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
   }
 }
 
-// bf16 head layout: 1 = quad layout (softmax_pool_bf16q_kernel), 0 = 8-channel layout;
+// bf16 head layout: 1 = quad layout (softmax_pool_bf16q_kernel, default: C3 +0.6 %,
+// profiles/r04/ab_c3_head_quads.txt), 0 = 8-channel layout;
 // pipnet_head_bf16_quads or PIPNET_HEAD_QUADS=0/1 switch it.
 #ifndef PIPNET_HEAD_QUADS_DEFAULT
-#define PIPNET_HEAD_QUADS_DEFAULT 0
+#define PIPNET_HEAD_QUADS_DEFAULT 1
 #endif
 static int g_head_quads = -1;
 static int head_quads() {

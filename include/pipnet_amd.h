@@ -94,7 +94,7 @@ int pipnet_gemm_persist(int mode);
  * (cached) stores, 0 = non-temporal (default); -1 queries.  Same bits either way.  Process-wide A/B
  * switch, not thread-safe against concurrent launches. */
 /* Layout of the bf16 prototype head (pipnet_softmax_pool_bf16): 1 = 4 channels per lane (8-B
- * loads, 16-B proto stores covering whole lines), 0 = 8 channels per lane (default); -1 queries.
+ * loads, 16-B proto stores covering whole lines; default), 0 = 8 channels per lane; -1 queries.
  * The softmax denominators' partial sums group differently (last-bit differences).  Process-wide
  * A/B switch, not thread-safe against concurrent launches. */
 int pipnet_head_bf16_quads(int mode);
