@@ -3,6 +3,7 @@
 #include "../count_pipnet_amd/csrc/convnext_dw.hpp"
 #include "dw_ring_lab.hpp"
 #include "dw_lds_lab.hpp"
+#include "dw_lnr_lab.hpp"
 using namespace pipnet_dw;
 
 extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, const float* wp, const float* bias,
@@ -21,6 +22,14 @@ extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, c
   // v8-v10: narrower column tiles for small maps (a row tile of G * TX pixels against W = 32 / 16)
   V(8, 96, 4, 1, 1, 8) V(8, 192, 4, 1, 1, 16) V(9, 96, 4, 2, 1, 8) V(9, 192, 4, 2, 1, 16)
   V(10, 96, 2, 2, 1, 8) V(10, 192, 2, 2, 1, 16)
+  // v50-v53 (round 4): the v40-v43 tiles with the LayerNorm in registers (dw_lnr_lab.hpp)
+#define LN(ID, CC, TX, TY) \
+  if (variant == ID && C == CC) return launch_dw_lnr<CC, TX, TY, 1>(x, B, H, W, wp, bias, lnw, lnb, y, s);
+  LN(50, 96, 7, 2) LN(50, 192, 7, 2) LN(50, 384, 7, 2) LN(50, 768, 7, 2)
+  LN(51, 96, 7, 3) LN(51, 192, 7, 3) LN(51, 384, 7, 3) LN(51, 768, 7, 3)
+  LN(52, 96, 4, 2) LN(52, 192, 4, 2) LN(52, 384, 4, 2) LN(52, 768, 4, 2)
+  LN(53, 96, 4, 4) LN(53, 192, 4, 4) LN(53, 384, 4, 4) LN(53, 768, 13, 1)
+#undef LN
   // v40-v43 (round 4): taller tiles now that each weight row is loaded once per workgroup
   V(40, 96, 7, 2, 1, 8) V(40, 192, 7, 2, 1, 16) V(40, 384, 7, 2, 1, 32) V(40, 768, 7, 2, 1, 64)
   V(41, 96, 7, 3, 1, 8) V(41, 192, 7, 3, 1, 16) V(41, 384, 7, 3, 1, 32) V(41, 768, 7, 3, 1, 64)
