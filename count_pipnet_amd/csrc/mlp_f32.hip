@@ -58,23 +58,17 @@ struct MlpGeo {
 // The product (pipnet_cnblock_mlp_hw_f32) takes HS = 2 for C = 192 on maps of at most
 // MLP_HS2_MAX_HW pixels per image (C5's stage 2 and C1: 16x16 / 8x8 maps) and HS = 1 otherwise
 // (C2's 28x28 stage 2, every C = 96 stage; profiles/r02/mlp_lab.txt, profiles/r03/bench_mlp_hs2.log).
-// ST = staggered wave halves (guide: MI355X_MICROARCH.md "Two waves per SIMD", item 9): waves
-// NW/2.. (the second wave of every SIMD pair) run each chunk's GEMM2 one chunk period late --
-// GEMM2(ci-1) then GEMM1(ci) + GELU in period ci, the GELU'd hidden block kept in registers across
-// the barrier -- so the two waves of a SIMD reach their GELU (VALU, MFMA pipe idle) at different
-// times instead of together after every chunk barrier.  Three LDS stages (W2 of chunk ci-1 stays
-// valid through period ci), one extra barrier period at the end.  Every wave sums the same terms
-// in the same order: bitwise the unstaggered kernel's output.  Lab only (tools/mlp_lab.hip): no
-// faster on any C2 / C5 shape, so the product launches ST = false (profiles/r04/mlp_stagger_lab.txt).
-template <int C, int HC, int NW, int PX, int HS = 1, bool ST = false>
+// (A staggered-halves form -- the second wave of each SIMD pair one chunk period late, so the two
+// waves' GELUs do not coincide -- was bitwise equal and no faster on any C2 / C5 shape in round 4;
+// profiles/r04/mlp_stagger_lab.txt.)
+template <int C, int HC, int NW, int PX, int HS = 1>
 __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
                                                               const float* __restrict__ W2,
                                                               const float* __restrict__ b2,
                                                               const float* __restrict__ gamma, float* x, int M) {
   using G = MlpGeo<C, HC, NW, PX, HS>;
-  constexpr int NSTG = ST ? 3 : 2;
-  static_assert(!ST || NW % 2 == 0, "stagger: two wave halves");
+  constexpr int NSTG = 2;
   // one LDS array (a second __shared__ object can make hipcc drain the DMA early): NSTG stage
   // buffers (HS chunks each), then b1 (staged once: a per-chunk global load of it would wait
   // for the DMA)
@@ -147,72 +141,6 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   };
   constexpr int NHB = HC / 16;
 
-  if constexpr (ST) {
-    // ---- staggered halves (see above): period ci = barrier, DMA of chunk ci+1, then
-    // half 0: GEMM1(ci) + GELU + GEMM2(ci); half 1: GEMM2(ci-1) + GEMM1(ci) + GELU ----
-    const bool late = __builtin_amdgcn_readfirstlane(wid) >= NW / 2;
-    f32x4 hk[PX][NHB];                                    // half 1: GELU'd hidden of the previous chunk
-    auto gemm1_gelu = [&](const float* buf, int ci, f32x4 (&h)[PX][NHB]) {
-      const int ch = part * G::NCHH + ci;
-#pragma unroll
-      for (int u = 0; u < PX; ++u)
-#pragma unroll
-        for (int hb = 0; hb < NHB; ++hb) h[u][hb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int g = 0; g < C / 16; ++g) {
-        f32x4 w[NHB];
-#pragma unroll
-        for (int hb = 0; hb < NHB; ++hb) w[hb] = ld4(buf + w1_off(hb, g));
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int hb = 0; hb < NHB; ++hb)
-#pragma unroll
-            for (int u = 0; u < PX; ++u)
-              h[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[hb][s], tb[u][g][s], h[u][hb], 0, 0, 0);
-      }
-#pragma unroll
-      for (int hb = 0; hb < NHB; ++hb) {
-        const f32x4 bb = ld4(sb1 + ch * HC + 16 * hb + 4 * q);
-#pragma unroll
-        for (int u = 0; u < PX; ++u) {
-          const f32x4 v = h[u][hb] + bb;
-          const f32x2 lo = gelu_pk16(f32x2{v[0], v[1]}), hi = gelu_pk16(f32x2{v[2], v[3]});
-          h[u][hb] = f32x4{lo[0], lo[1], hi[0], hi[1]};
-        }
-      }
-    };
-    auto gemm2 = [&](const float* buf, const f32x4 (&h)[PX][NHB]) {
-#pragma unroll
-      for (int hb = 0; hb < NHB; ++hb) {
-        f32x4 w[C / 16];
-#pragma unroll
-        for (int cb = 0; cb < C / 16; ++cb) w[cb] = ld4(buf + w2_off(cb, hb));
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int cb = 0; cb < C / 16; ++cb)
-#pragma unroll
-            for (int u = 0; u < PX; ++u)
-              acc[u][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[cb][s], h[u][hb][s], acc[u][cb], 0, 0, 0);
-      }
-    };
-    for (int ci = 0; ci <= G::NCHH; ++ci) {
-      // this wave's pieces of chunk ci landed; every wave is past period ci-1, so chunk ci-2's
-      // buffer -- the DMA target of chunk ci+1 -- has no reader left
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (ci + 1 < G::NCHH) stage(ci + 1);
-      const float* buf = smem + (ci % 3) * G::STAGE_F + part * G::CHUNK_F;
-      const float* prev = smem + ((ci + 2) % 3) * G::STAGE_F + part * G::CHUNK_F;   // chunk ci-1
-      // one GEMM1 + GELU site for both halves; GEMM2 of the late half before it (chunk ci-1),
-      // of the early half after it (chunk ci)
-      if (late && ci > 0) gemm2(prev, hk);
-      if (ci < G::NCHH) {
-        gemm1_gelu(buf, ci, hk);
-        if (!late) gemm2(buf, hk);
-      }
-    }
-  } else
   for (int ci = 0; ci < G::NCHH; ++ci) {
     // this wave's pieces of stage ci landed, every wave's reads of stage ci-1 retired
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -303,11 +231,11 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
   }
 }
 
-template <int C, int HC, int NW, int PX, int HS = 1, bool ST = false>
+template <int C, int HC, int NW, int PX, int HS = 1>
 int launch_mlp(const float* t, const float* W1, const float* b1, const float* W2, const float* b2, const float* gamma,
                float* x, int M, hipStream_t s) {
   const int px = 16 * PX * NW / HS;
-  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX, HS, ST>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1,
+  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX, HS>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1,
                      b1, W2, b2, gamma, x, M);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;

@@ -568,17 +568,16 @@ MLP_HS2_MAX_HW = 256    # C = 192 on maps of <= 16 x 16: hidden split over two w
 
 
 def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20, hw: int = 0) -> str:
-    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32; the last
-    template argument is the lab-only staggered form, never launched by the product)."""
+    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32)."""
     if c == 192 and 0 < hw <= MLP_HS2_MAX_HW:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 2, false>"
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
     if c == 96:
         nw = 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
-        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1, false>"
+        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
     if m >= 32768:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 1, false>"
+        return "cnblock_mlp_kernel<192, 16, 8, 1, 1>"
     nw = 4 if m >= 8192 else 2 if m >= 4096 else 1
-    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1, false>"
+    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
 
 
 def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor,

@@ -12,19 +12,14 @@ bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float*
 #define V(ID, CC, HC, NW, PX) V2(ID, CC, HC, NW, PX, 1)
 #define V2(ID, CC, HC, NW, PX, HS) \
   case ID: if (C != CC) return false; launch_mlp<CC, HC, NW, PX, HS>(t, W1, b1, W2, b2, gamma, x, M, s); return true;
-#define VS(ID, CC, HC, NW, PX, HS) \
-  case ID: if (C != CC) return false; launch_mlp<CC, HC, NW, PX, HS, true>(t, W1, b1, W2, b2, gamma, x, M, s); return true;
   switch (g_variant) {
     V(1, 96, 32, 8, 2) V(2, 96, 32, 4, 2) V(4, 96, 32, 4, 1) V(5, 96, 16, 4, 2)
     V(11, 192, 32, 8, 1) V(12, 192, 32, 4, 1) V(13, 192, 16, 8, 1) V(14, 192, 16, 2, 1)
     // hidden split over 2 waves per pixel group (HS = 2)
     V2(21, 192, 16, 8, 1, 2) V2(24, 192, 16, 4, 1, 2) V2(25, 192, 16, 2, 1, 2)
     V2(31, 96, 32, 8, 1, 2) V2(32, 96, 16, 8, 1, 2) V2(33, 96, 32, 4, 1, 2)
-    // staggered wave halves (round 4): the product instantiations with ST
-    VS(41, 96, 32, 8, 1, 1) VS(42, 192, 16, 8, 1, 2) VS(43, 192, 16, 8, 1, 1) VS(44, 96, 32, 4, 1, 1)
     default: return false;
   }
 #undef V
 #undef V2
-#undef VS
 }

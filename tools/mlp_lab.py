@@ -18,7 +18,7 @@ from count_pipnet_amd import build  # noqa: E402
 from count_pipnet_amd import kernels as K  # noqa: E402
 
 SO = os.path.join(HERE, "libmlp_lab.so")
-VARIANTS = {96: [0, 41, 44], 192: [0, 21, 42, 43]}
+VARIANTS = {96: [0], 192: [0, 21]}
 if os.environ.get("LAB_VARIANTS"):
     VARIANTS = json.loads(os.environ["LAB_VARIANTS"])
     VARIANTS = {int(k): v for k, v in VARIANTS.items()}
