@@ -28,7 +28,6 @@ SIGNATURES = {
     "pipnet_gemm_persist": [I32],
     "pipnet_gemm_stream": [I32],
     "pipnet_conv_bf16_rb": [I32],
-    "pipnet_conv_bf16_tile_rule": [I32],
     "pipnet_gemm_bk16x3": [I32],
     "pipnet_gemm_plain_store": [I32],
     "pipnet_head_bf16_quads": [I32],

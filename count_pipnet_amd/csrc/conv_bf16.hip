@@ -37,7 +37,6 @@ using CfgL = Cfg<2, 4, 4, 2>;          // 256 x 256, 512 threads, 128 KiB LDS, 1
 using CfgL4 = Cfg<2, 4, 4, 2, 32, 4>;  // 256 x 256, BK 32 x 4 stages (3 tiles in flight), 128 KiB
 using CfgM4 = Cfg<2, 2, 2, 2, 32, 4>;  // 128 x 128, BK 32 x 4 stages, 64 KiB, 2 workgroups / CU
 using CfgN64 = Cfg<4, 1, 2, 2, 32, 4>; // 256 x 64 (N = 64 layers), BK 32 x 4 stages, 80 KiB, 2 workgroups / CU
-using CfgM3 = Cfg<2, 2, 2, 2, 32, 3>;  // 128 x 128, BK 32 x 3 stages, 48 KiB, 3 workgroups / CU (tile 12)
 
 // Tile choice: the largest tile that still gives every CU at least one workgroup (larger
 // tiles halve the L2 -> LDS bytes per MFMA: 128x128 needs ~64 B/clk/CU at the MFMA rate,
@@ -48,18 +47,7 @@ using CfgM3 = Cfg<2, 2, 2, 2, 32, 3>;  // 128 x 128, BK 32 x 3 stages, 48 KiB, 3
 // Mirrored by kernels.py:bf16_conv_tile.
 // N >= 256 layers run the ping-pong 16x16x32 kernel (tile 5) at every batch size -- the
 // choice depends on the layer only, never on M, so per-pixel results stay batch-invariant.
-// Round-4 tile rule (tile 12 and the short-K conv3 + identity rule below): 1 = on (default), 0 =
-// round 3's rule; pipnet_conv_bf16_tile_rule or PIPNET_CONV_TILE_RULE=0/1 switch it (A/B runs).
-int g_tile_rule = -1;
-int tile_rule() {
-  if (g_tile_rule < 0) {
-    const char* e = getenv("PIPNET_CONV_TILE_RULE");
-    g_tile_rule = e ? (e[0] == '1') : 1;
-  }
-  return g_tile_rule;
-}
-
-int conv_variant(int M, int N, bool pp_ok, bool s3 = false, int Kv = 0, bool resid = false) {
+int conv_variant(int M, int N, bool pp_ok, bool s3 = false, int Kv = 0) {
   if (s3) {  // split GEMMs (tools/s3_tiles.py, profiles/r01/s3_tiles.txt); tiles 0 / 4 / 5 / 7 only
     const int m128 = ((M + 127) / 128) * ((N + 127) / 128) >= 512 ? 4 : 0;
     if (!pp_ok) return m128;
@@ -71,22 +59,14 @@ int conv_variant(int M, int N, bool pp_ok, bool s3 = false, int Kv = 0, bool res
   // K <= 64 (layer1 conv3: 64 -> 256 + identity): one K-tile pair per tile, all epilogue -- the
   // 2-workgroup 128 x 128 tile overlaps one workgroup's epilogue with the other's MFMAs
   // (41 vs 47 us per half batch, profiles/r03/conv_bf16_b64.log).  A per-layer rule (K, N).
-  // conv3 + identity with K <= 256 (layer2 / layer3 conv3): the identity read and the output
-  // store make the single-workgroup ping-pong tiles epilogue-bound (one workgroup per CU: nothing
-  // runs on the matrix pipe meanwhile); three 128 x 128 workgroups per CU (tile 12) overlap one
-  // workgroup's epilogue with the others' MFMAs -- l3.c3 71 -> 51 us, l2.c3 31 -> 28 us at 64
-  // images (profiles/r04/conv_bf16_tile12.log).  A per-layer rule (epilogue, K).
-  const bool r4 = tile_rule() != 0;
-  const bool resid_short = r4 && resid && Kv <= 256;
-  if (N >= 256 && pp_ok && Kv > 64 && !resid_short) return 5;
+  if (N >= 256 && pp_ok && Kv > 64) return 5;
   if (N <= 64 && !s3) return 6;   // 256 x 64: a 128-wide tile would compute half padding columns
   const int64_t tl = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
-  if (N >= 256 && tl >= 256 && Kv > 64 && !resid_short) return 3;
+  if (N >= 256 && tl >= 256 && Kv > 64) return 3;
   // 128 x 128 once the grid covers each CU once (layer2 conv2 at 64 images: 392 tiles, 31-34 vs
-  // 42-44 us on 64 x 128), three workgroups per CU (tile 12: 48 KiB of LDS in 3 stages; 3-10 %
-  // over tile 4's two, profiles/r04/conv_bf16_tile12.log); tiles 0 / 3 / 4 / 12 walk K
-  // identically, so this M-dependent choice keeps every pixel's result bitwise batch-invariant
-  if (tm >= 256) return s3 || !r4 ? 4 : 12;
+  // 42-44 us on 64 x 128); tiles 0 / 3 / 4 walk K identically, so this M-dependent choice keeps
+  // every pixel's result bitwise batch-invariant
+  if (tm >= 256) return 4;
   return 0;
 }
 
@@ -166,12 +146,12 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   // 1x1 convs with N % 256 == 0: the persistent ping-pong tile (9), same K order as tile 5
   const bool pk = ALOAD == ALOAD_DENSE && pp_ok && p.N % 256 == 0 && !is_s3_epi(epi);
   if (v < 0) {
-    v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv > 0 ? p.Kv : p.K, epi == PIPNET_EPI_BIAS_RESID_RELU);
+    v = conv_variant(p.M, p.N, pp_ok, is_s3_epi(epi), p.Kv > 0 ? p.Kv : p.K);
     if (hk) v = 8;
     else if (h64 && H64_AUTO) v = 11;
     else if (v == 5 && pk) v = 9;
   }
-  if (v > 12 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
+  if (v > 11 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
   if (v == 11) {                                 // Cin = N = 64 / 128 3x3 on the LDS input halo
     const int bm = p.N == 64 ? hsm::Shape<64>::BM : hsm::Shape<128>::BM;
     p.nt = 1;
@@ -308,7 +288,6 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     else if (v == 4) hipLaunchKernelGGL((conv_bf16_kernel<CfgM4, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else if (v == 6) hipLaunchKernelGGL((conv_bf16_kernel<CfgN64, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
     else if (v == 1) hipLaunchKernelGGL((conv_bf16_kernel<CfgM, E, ALOAD, 2>), grid, dim3(256), 0, s, p); \
-    else if (v == 12) hipLaunchKernelGGL((conv_bf16_kernel<CfgM3, E, ALOAD, 3>), grid, dim3(256), 0, s, p); \
     else hipLaunchKernelGGL((conv_bf16_kernel<CfgS, E, ALOAD, 3>), grid, dim3(256), 0, s, p);        \
     break;
   // split-bf16 epilogues: only the tiles the automatic choice picks for N < 256 (0 and 4)
@@ -466,12 +445,6 @@ extern "C" int pipnet_conv_bf16_rb(int mode) {
   if (rb_mode_ok(mode)) g_pp_rb = mode;
   else if (mode != -1) return -PIPNET_ERR_ARG;
   return pp_rb_mode();
-}
-
-extern "C" int pipnet_conv_bf16_tile_rule(int mode) {
-  if (mode == 0 || mode == 1) g_tile_rule = mode;
-  else if (mode != -1) return -PIPNET_ERR_ARG;
-  return tile_rule();
 }
 
 extern "C" int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias,

@@ -307,17 +307,8 @@ def _chk_bf(t: Tensor, what: str) -> None:
         raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
 
 
-def conv_bf16_tile_rule(mode: int = -1) -> int:
-    """The library's bf16 conv tile-rule switch (include/pipnet_amd.h pipnet_conv_bf16_tile_rule):
-    1 = round 4's rule (default), 0 = round 3's, -1 queries."""
-    r = _lib.load().pipnet_conv_bf16_tile_rule(mode)
-    if r < 0:
-        _lib.check(-r, f"pipnet_conv_bf16_tile_rule({mode})")
-    return r
-
-
 def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int = 0, halo_ok: bool = False,
-                   ppp_ok: bool = False, halo64_ok: bool = False, resid: bool = False) -> int:
+                   ppp_ok: bool = False, halo64_ok: bool = False) -> int:
     """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
     11 = 3x3 stride-1 pad-1 Cin = N = 64 (W <= 63) / 128 (W <= 31) convs on an LDS input halo (the
@@ -326,9 +317,7 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
     5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
     6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 / 8 / 9 on
     32x32x16 MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M.
-    12 = 128x128 with three workgroups per CU (every tile-4 choice outside the split-bf16 path).
-    ``kv`` = KH*KW*Cin: layers with K <= 64, and conv3 + identity (``resid``) with K <= 256, never
-    take the single-workgroup ping-pong tiles."""
+    ``kv`` = KH*KW*Cin: layers with K <= 64 never take the single-workgroup ping-pong tiles."""
     if s3:
         m128 = 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
         if not pp_ok:
@@ -342,21 +331,19 @@ def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int
         return 8
     if halo64_ok:
         return 11
-    r4 = (conv_bf16_tile_rule(-1) if torch.cuda.is_available() else 1) != 0
-    short_k = 0 < kv <= 64 or (r4 and resid and kv <= 256)     # multi-workgroup tiles (conv_variant)
+    short_k = 0 < kv <= 64                  # layer1 conv3 / downsample (K = 64): 2-workgroup tiles
     if n >= 256 and pp_ok and not short_k:
         return 9 if ppp_ok else 5
     if n <= 64 and not s3:
         return 6
     if n >= 256 and -(-m // 256) * -(-n // 256) >= 256 and not short_k:
         return 3
-    return (12 if r4 else 4) if -(-m // 128) * -(-n // 128) >= 256 else 0
+    return 4 if -(-m // 128) * -(-n // 128) >= 256 else 0
 
 
 _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
              2: ("pipnet_bf16::Cfg<2, 4, 4, 2, 64, 2>", 1), 3: ("pipnet_bf16::Cfg<2, 4, 4, 2, 32, 4>", 1),
-             4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2), 6: ("pipnet_bf16::Cfg<4, 1, 2, 2, 32, 4>", 2),
-             12: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 3>", 3)}
+             4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2), 6: ("pipnet_bf16::Cfg<4, 1, 2, 2, 32, 4>", 2)}
 
 
 def conv_bf16_rb(mode: int = -1) -> int:
@@ -390,8 +377,7 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
                           s3: bool = False, kv: int = 0, halo_ok: bool = False, ppp_ok: bool = False,
                           halo64_ok: bool = False) -> str:
     """rocprof name of the bf16 conv instantiation."""
-    t = (bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok, halo64_ok, resid=epilogue == _lib.EPI_BIAS_RESID_RELU)
-         if tile < 0 else tile)
+    t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok, halo64_ok) if tile < 0 else tile
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
@@ -456,7 +442,7 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
                  and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     if halo64_ok and tile < 0 and not CONV3X3_N64_HALO:
         halo64_ok = False                   # the same arithmetic on the generic tile
-        tile = 6 if cout == 64 else bf16_conv_tile(m, cout, pp_ok, kv=k, resid=epilogue == _lib.EPI_BIAS_RESID_RELU)
+        tile = 6 if cout == 64 else bf16_conv_tile(m, cout, pp_ok, kv=k)
     _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok,
                                   halo64_ok=halo64_ok),
             2.0 * m * cout * k,

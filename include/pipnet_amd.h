@@ -506,12 +506,6 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
  * Process-wide A/B switch, not thread-safe against concurrent launches. */
 int pipnet_conv_bf16_rb(int mode);
 
-/* bf16 conv tile rule: 1 = round 4's (default: every two-workgroup 128x128 choice on the
- * three-workgroup tile 12, and conv3 + identity with K <= 256 off the single-workgroup ping-pong
- * tiles), 0 = round 3's; -1 queries.  Returns the mode or -PIPNET_ERR_ARG.  Process-wide A/B
- * switch, not thread-safe against concurrent launches. */
-int pipnet_conv_bf16_tile_rule(int mode);
-
 /* fp64-accumulated product for inference-time weight folds (csrc/fold_f64.hip):
  *   C[M,N] (ldc) = RNE_f32( sum_k double(A[m,k]) * double(B[k,n]) ), A [M,K] (lda) and B [K,N]
  *   (ldb) row-major fp32, products and sums in fp64 on v_mfma_f64_16x16x4_f64, any sizes.

@@ -525,25 +525,3 @@ def test_head_bf16_quad_layout(gpu, b, hw, p):
         torch.testing.assert_close(pooled, ref.amax(dim=1), rtol=1e-5, atol=1e-7)
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=2e-6, atol=1e-9)
     assert K.head_bf16_quads(-1) == prev
-
-
-@pytest.mark.parametrize("m,cin,cout,k,epi", [(4704, 256, 128, 1, _lib.EPI_BIAS_RELU), (3000, 64, 256, 1, _lib.EPI_BIAS_RESID_RELU),
-                                              (2, 128, 128, 3, _lib.EPI_BIAS), (777, 512, 64, 1, _lib.EPI_NONE)])
-def test_tile12_bitwise_equals_tile4(gpu, m, cin, cout, k, epi):
-    """Tile 12 (128x128, 32-deep K x 3 stages, three workgroups per CU) walks K exactly as
-    tile 4 (4 stages, two per CU): bit-identical outputs, ragged M and N included."""
-    gg = torch.Generator().manual_seed(5)
-    if k == 1:
-        x = torch.randn(1, m, 1, cin, generator=gg).to(torch.bfloat16).to(gpu)
-        r = torch.randn(1, m, 1, cout, generator=gg).to(torch.bfloat16).to(gpu)
-        pad = 0
-    else:
-        x = torch.randn(m, 28, 28, cin, generator=gg).to(torch.bfloat16).to(gpu)
-        r = None
-        pad = 1
-    w = K.pack_conv_weight_bf16((torch.randn(cout, k, k, cin, generator=gg) / (k * cin ** 0.5)).to(gpu))
-    b = torch.randn(cout, generator=gg).to(gpu)
-    outs = [K.conv2d_nhwc_bf16(x, w, k, k, None if epi == _lib.EPI_NONE else b, 1, pad, epi,
-                               r if epi == _lib.EPI_BIAS_RESID_RELU else None, tile=t) for t in (4, 12)]
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])

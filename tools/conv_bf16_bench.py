@@ -66,8 +66,7 @@ def main():
         halo = k == 3 and s == 1 and pad == 1 and cin % 64 == 0 and oh <= 31 and cout >= 256
         ppp = k == 1 and s == 1 and pad == 0 and cout % 256 == 0
         h64 = k == 3 and s == 1 and pad == 1 and cin == cout and ((cin == 64 and oh <= 63) or (cin == 128 and oh <= 31))
-        auto = K.bf16_conv_tile(a.batch * oh * oh, cout, kv=k * k * cin, halo_ok=halo, ppp_ok=ppp, halo64_ok=h64,
-                                resid=epi == _lib.EPI_BIAS_RESID_RELU)
+        auto = K.bf16_conv_tile(a.batch * oh * oh, cout, kv=k * k * cin, halo_ok=halo, ppp_ok=ppp, halo64_ok=h64)
         line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={auto}"
         for t in tiles:
             if isinstance(t, str):          # --rb-ab: automatic tile, row-block mode r8 / rA
