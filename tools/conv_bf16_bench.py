@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--rb-ab", action="store_true",
                     help="time the automatic tile twice: 256-row ping-pong tiles forced (r8) and the automatic "
                          "224/256-row choice (rA) -- kernels.conv_bf16_rb")
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="cycle through this many input / identity / output buffer sets, so a layer's "
+                         "working set exceeds the 256 MB Infinity Cache as it does in the network")
     ap.add_argument("--lib", action="store_true",
                     help="also time the vendor library on the same shape (torch bf16: hipBLASLt GEMM for 1x1 "
                          "convs, MIOpen channels_last conv otherwise) as a reference ceiling")
@@ -57,11 +60,13 @@ def main():
     for name, h, cin, cout, k, s, pad, epi, cnt in LAYERS:
         if a.only and name not in a.only.split(","):
             continue
-        x = torch.randn(a.batch, h, h, cin, device=dev).to(torch.bfloat16)
+        xs = [torch.randn(a.batch, h, h, cin, device=dev).to(torch.bfloat16) for _ in range(a.rotate)]
         w = K.pack_conv_weight_bf16(torch.randn(cout, k, k, cin, device=dev) * 0.05)
         b = torch.randn(cout, device=dev)
         oh = (h + 2 * pad - k) // s + 1
-        r = torch.randn(a.batch, oh, oh, cout, device=dev).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU else None
+        rs = [torch.randn(a.batch, oh, oh, cout, device=dev).to(torch.bfloat16) if epi == _lib.EPI_BIAS_RESID_RELU
+              else None for _ in range(a.rotate)]
+        x, r = xs[0], rs[0]
         flops = 2.0 * a.batch * oh * oh * cout * k * k * cin
         halo = k == 3 and s == 1 and pad == 1 and cin % 64 == 0 and oh <= 31 and cout >= 256
         ppp = k == 1 and s == 1 and pad == 0 and cout % 256 == 0
@@ -81,8 +86,8 @@ def main():
                 continue
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(a.reps):
-                K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=ti)
+            for i in range(a.reps):
+                K.conv2d_nhwc_bf16(xs[i % a.rotate], w, k, k, b, s, pad, epi, rs[i % a.rotate], tile=ti)
             e1.record()
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / a.reps
