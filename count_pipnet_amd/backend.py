@@ -63,3 +63,14 @@ def invalidate_weight_caches(net: torch.nn.Module) -> int:
                 c.clear()
                 n += 1
     return n
+
+
+def packed_ready() -> None:
+    """Call right after a weight cache was (re)built: the repacking kernels ran on the current
+    stream, and a concurrent sub-batch forward on another HIP stream (pipnet.set_stream_split)
+    would read the new buffers without waiting for them.  Host-synchronises the current stream
+    on a cache miss only (first forward, or after a weight change), never during graph capture
+    (captures replay warm caches)."""
+    if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream().synchronize()
+

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import kernels as K
-from .backend import use_hip
+from .backend import use_hip, packed_ready
 
 Tensor = torch.Tensor
 
@@ -118,6 +118,11 @@ class ConvNeXt(nn.Module):
                     nn.init.zeros_(m.bias)
         self._hip_pack: Dict = {}
 
+    def hip_steps(self, x: Tensor):
+        """The HIP forward as a block-by-block generator returning NHWC features."""
+        return convnext_features_hip_steps(self.features, x, self._hip_pack,
+                                           precision=getattr(self, "hip_precision", "fp32"))
+
     def forward(self, x: Tensor) -> Tensor:
         if use_hip(self):
             return nhwc_as_nchw(convnext_features_hip(self.features, x, self._hip_pack,
@@ -168,6 +173,11 @@ class MidLayerConvNeXt(nn.Module):
             for i in range(min(num_stages, len(original_model.features) - 1)):
                 self.features.add_module(str(i + 1), original_model.features[i + 1])
         self._hip_pack: Dict = {}
+
+    def hip_steps(self, x: Tensor):
+        """The HIP forward as a block-by-block generator returning NHWC features."""
+        return convnext_features_hip_steps(self.features, x, self._hip_pack,
+                                           precision=getattr(self, "hip_precision", "fp32"))
 
     def forward(self, x: Tensor) -> Tensor:
         if use_hip(self):
@@ -231,6 +241,7 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
         with torch.no_grad():
             ent = (stamp, fn(t.detach()).contiguous())
         cache[key] = ent
+        packed_ready()
     return ent[1]
 
 
@@ -324,7 +335,26 @@ def stochastic_depth_row_scales(features: nn.Sequential, sd_keep: Dict[int, obje
 
 def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
                           sd_keep: Optional[Dict[int, object]] = None, precision: str = "fp32") -> Tensor:
-    """Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels.
+    """Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels
+    (convnext_features_hip_steps, drained)."""
+    return drain(convnext_features_hip_steps(features, x, cache, sd_keep, precision))
+
+
+def drain(steps):
+    """Run a ``*_hip_steps`` generator to completion; its return value."""
+    while True:
+        try:
+            next(steps)
+        except StopIteration as e:
+            return e.value
+
+
+def convnext_features_hip_steps(features: nn.Sequential, x: Tensor, cache: Dict,
+                                sd_keep: Optional[Dict[int, object]] = None, precision: str = "fp32"):
+    """Generator form of convnext_features_hip: yields after the stem, every CNBlock and every
+    downsample (the launches of that stage are enqueued by then), returns the NHWC features --
+    so concurrent sub-batch forwards can enqueue block by block (pipnet._forward_hip_split).
+    Run a (possibly truncated, stride-patched) ConvNeXt ``features`` on the HIP kernels.
     ``sd_keep``: train-mode stochastic depth, block id (0..17 in module order) -> per-sample
     keep mask for every block with p > 0 (eval / None: no stochastic depth).
     ``precision``: "fp32" (exact fp32 MFMA GEMMs) or "bf16x3" (the CNBlock Linears and the
@@ -345,6 +375,7 @@ def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
             if conv.kernel_size != (4, 4) or conv.stride != (4, 4) or conv.in_channels != 3 or conv.out_channels != 96:
                 raise RuntimeError(f"unsupported ConvNeXt stem {conv}")
             h = K.convnext_stem(x, conv.weight, conv.bias, ln.weight, ln.bias)
+            yield
         elif len(mod) > 0 and isinstance(mod[0], CNBlock):
             for j, blk in enumerate(mod):
                 if s3:
@@ -352,6 +383,7 @@ def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
                 else:
                     h = _cnblock_hip(blk, h, cache, f"{name}.{j}", None if scales is None else scales.get(bid))
                 bid += 1
+                yield
         elif len(mod) == 2 and isinstance(mod[0], LayerNorm2d) and isinstance(mod[1], nn.Conv2d):
             ln, conv = mod[0], mod[1]
             if conv.kernel_size != (2, 2) or conv.padding != (0, 0):
@@ -365,6 +397,7 @@ def convnext_features_hip(features: nn.Sequential, x: Tensor, cache: Dict,
                 t = K.layernorm(h, ln.weight, ln.bias)
                 wp = packed(cache, name + ".conv", conv.weight, lambda w: w.permute(0, 2, 3, 1))
                 h = K.conv2x2(t, wp, conv.bias, conv.stride[0])
+            yield
         else:
             raise RuntimeError(f"unsupported ConvNeXt features entry {idx}: {type(mod).__name__}")
     return h

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import kernels as K
-from .backend import use_hip
+from .backend import packed_ready, use_hip
 from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
 from .count_pipnet_utils import (BilinearIntermediate, ClampSTE, GumbelSoftmax, IdentityIntermediate,
                                  LinearFull, LinearIntermediate, OneHotEncoder, STE_Round)
@@ -223,6 +223,7 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
             vf = K.matmul_f64acc(layer.V.weight.detach().contiguous(), e)
         ent = (stamp, (wf, vf))
         cache[key] = ent
+        packed_ready()
     return ent[1]
 
 

@@ -95,11 +95,33 @@ class PIPNet(nn.Module):
         main = torch.cuda.current_stream(dev)
         streams = _side_streams(dev, n)
         parts = xs.chunk(n)
-        logits = []
-        for s, p in zip(streams, parts):
+        for s in streams:
             s.wait_stream(main)
-            with torch.cuda.stream(s):
-                logits.append(self._hip_logits(p))
+        net = self._net
+        if INTERLEAVE and hasattr(net, "hip_steps") and use_hip(net):
+            # enqueue the sub-batch forwards block by block, round robin, so every stream has
+            # work from the start (enqueued one after the other, the second stream trailed the
+            # first by the host's enqueue time of a whole backbone)
+            gens = [net.hip_steps(p) for p in parts]
+            feats = [None] * n
+            live = list(range(n))
+            while live:
+                for i in list(live):
+                    with torch.cuda.stream(streams[i]):
+                        try:
+                            next(gens[i])
+                        except StopIteration as e:
+                            feats[i] = e.value
+                            live.remove(i)
+            logits = []
+            for s, f in zip(streams, feats):
+                with torch.cuda.stream(s):
+                    logits.append(add_on_logits_hip(self._add_on, f))
+        else:
+            logits = []
+            for s, p in zip(streams, parts):
+                with torch.cuda.stream(s):
+                    logits.append(self._hip_logits(p))
         b = xs.shape[0]
         _, h, w, pn = logits[0].shape
         k = self._classification.weight.shape[0]
@@ -128,6 +150,9 @@ class PIPNet(nn.Module):
 # -- profiles/r03/stream_split_ab.txt.  bench.py takes per-kernel roofline timings from a
 # separate one-stream pass, where each launch runs alone.
 STREAM_SPLIT_MIN_BATCH = 32
+# Sub-batch forwards enqueued block by block, round robin (backbones with ``hip_steps``), rather
+# than one whole backbone after the other.
+INTERLEAVE = True
 _SIDE_STREAMS = {}
 
 

@@ -129,6 +129,11 @@ class ResNet_features(nn.Module):
             self.paddings += ps
         return nn.Sequential(*blocks)
 
+    def hip_steps(self, x):
+        """The HIP forward as a block-by-block generator returning NHWC features."""
+        from .resnet_hip import resnet_features_hip_steps
+        return resnet_features_hip_steps(self, x, self._hip_pack)
+
     def forward(self, x):
         if use_hip(self):
             from .resnet_hip import resnet_features_hip

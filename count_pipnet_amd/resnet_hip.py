@@ -24,6 +24,7 @@ from typing import Dict, Optional
 import torch
 import torch.nn as nn
 
+from .backend import packed_ready
 from . import _lib
 from . import kernels as K
 
@@ -53,6 +54,7 @@ def _fold(cache: Dict, key: str, conv: nn.Conv2d, bn: nn.BatchNorm2d, cpad: Opti
                 w = K.pack_conv_weight_bf16(w)
             ent = (stamp, (w, b.contiguous().float()))
         cache[ck] = ent
+        packed_ready()
     return ent[1]
 
 
@@ -66,6 +68,7 @@ def _stem_s2d(cache: Dict, conv: nn.Conv2d, bn: nn.BatchNorm2d):
         with torch.no_grad():
             ent = (w, K.pack_conv_weight_bf16(K.stem_weight_s2d(w)))
         cache[ck] = ent
+        packed_ready()
     return ent[1], b
 
 
@@ -107,6 +110,7 @@ def _dual_weights(cache, key, blk):
         with torch.no_grad():
             ent = ((wd, w1), (torch.cat([wd, w1]).contiguous(), torch.cat([bd, b1]).contiguous()))
         cache[ck] = ent
+        packed_ready()
     return ent[1][0], ent[1][1], wd.shape[0], w1.shape[0]
 
 
@@ -134,7 +138,16 @@ def _bottleneck(cache, key, blk, h):
 
 def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
     """ResNet_features.forward (resnet_features.py:211-222) on HIP kernels -> NHWC features
-    (fp32, or bf16 when ``model.hip_dtype`` is torch.bfloat16)."""
+    (fp32, or bf16 when ``model.hip_dtype`` is torch.bfloat16); resnet_features_hip_steps,
+    drained."""
+    from .convnext_features import drain
+    return drain(resnet_features_hip_steps(model, x, cache))
+
+
+def resnet_features_hip_steps(model, x: Tensor, cache: Dict):
+    """Generator form of resnet_features_hip: yields after the stem and after every block
+    (their launches enqueued), returns the NHWC features -- concurrent sub-batch forwards
+    enqueue block by block (pipnet._forward_hip_split)."""
     K.require_device(x, "network input")
     x = x.contiguous()
     if x.shape[1] != 3:
@@ -161,7 +174,9 @@ def resnet_features_hip(model, x: Tensor, cache: Dict) -> Tensor:
         h = K.nchw_to_nhwc(x, 4)
         h = _conv_bn(cache, "stem", model.conv1, model.bn1, h, _lib.EPI_BIAS_RELU, cpad=4)
         h = K.maxpool2d_nhwc(h, 3, 2, 1)
+    yield
     for li, layer in enumerate((model.layer1, model.layer2, model.layer3, model.layer4)):
         for j, blk in enumerate(layer):
             h = _bottleneck(cache, f"layer{li + 1}.{j}", blk, h)
+            yield
     return h
