@@ -24,7 +24,8 @@ from .backend import packed_ready, use_hip
 from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
 from .count_pipnet_utils import (BilinearIntermediate, ClampSTE, GumbelSoftmax, IdentityIntermediate,
                                  LinearFull, LinearIntermediate, OneHotEncoder, STE_Round)
-from .pipnet import _side_streams, add_on_logits_hip, stream_split
+from . import pipnet as _pipnet
+from .pipnet import _side_streams, add_on_logits_hip, interleaved_features, stream_split
 
 
 class CountPIPNet(nn.Module):
@@ -109,13 +110,20 @@ class CountPIPNet(nn.Module):
         parts = xs.chunk(n)
         act = list(self._add_on)[-1] if isinstance(self._add_on, nn.Sequential) else self._add_on
         gumbel = isinstance(act, GumbelSoftmax)
-        logits = []
-        for s, p in zip(streams, parts):
+        kind = GumbelSoftmax if gumbel else nn.Softmax
+        for s in streams:
             s.wait_stream(main)
+        if _pipnet.INTERLEAVE and hasattr(self._net, "hip_steps") and use_hip(self._net):
+            feats = interleaved_features(self._net, parts, streams)
+        else:
+            feats = []
+            for s, p in zip(streams, parts):
+                with torch.cuda.stream(s):
+                    feats.append(as_nhwc(self._net(p)))
+        logits = []
+        for s, f in zip(streams, feats):
             with torch.cuda.stream(s):
-                feats = as_nhwc(self._net(p))
-                logits.append(add_on_logits_hip(self._add_on, feats,
-                                                activation=GumbelSoftmax if gumbel else nn.Softmax))
+                logits.append(add_on_logits_hip(self._add_on, f, activation=kind))
         b = xs.shape[0]
         _, h, w, pn = logits[0].shape
         proto = torch.empty((b, h, w, pn), device=dev, dtype=torch.float32)

@@ -102,17 +102,7 @@ class PIPNet(nn.Module):
             # enqueue the sub-batch forwards block by block, round robin, so every stream has
             # work from the start (enqueued one after the other, the second stream trailed the
             # first by the host's enqueue time of a whole backbone)
-            gens = [net.hip_steps(p) for p in parts]
-            feats = [None] * n
-            live = list(range(n))
-            while live:
-                for i in list(live):
-                    with torch.cuda.stream(streams[i]):
-                        try:
-                            next(gens[i])
-                        except StopIteration as e:
-                            feats[i] = e.value
-                            live.remove(i)
+            feats = interleaved_features(net, parts, streams)
             logits = []
             for s, f in zip(streams, feats):
                 with torch.cuda.stream(s):
@@ -154,6 +144,23 @@ STREAM_SPLIT_MIN_BATCH = 32
 # than one whole backbone after the other.
 INTERLEAVE = True
 _SIDE_STREAMS = {}
+
+
+def interleaved_features(net, parts, streams):
+    """Backbone features of each sub-batch ``parts[i]`` on ``streams[i]``, enqueued one block at
+    a time, round robin over the streams (``net.hip_steps`` yields after every block)."""
+    gens = [net.hip_steps(p) for p in parts]
+    feats = [None] * len(parts)
+    live = list(range(len(parts)))
+    while live:
+        for i in list(live):
+            with torch.cuda.stream(streams[i]):
+                try:
+                    next(gens[i])
+                except StopIteration as e:
+                    feats[i] = e.value
+                    live.remove(i)
+    return feats
 
 
 def _side_streams(dev, n):
