@@ -49,7 +49,7 @@ def main():
         times = {}
         epis = [epi0 if e == "native" else int(e) for e in EPIS]
         cfgs = list(itertools.product(VARIANTS, GROUPS, epis))
-        for rnd in range(3):
+        for rnd in range(int(os.environ.get("LAB_ROUNDS", "3"))):
             for v, gm, epi in cfgs:
                 def run():
                     st = lib.lab_linear(v, gm, A.data_ptr(), k, W.data_ptr(), b.data_ptr(), s.data_ptr(), R.data_ptr(),
@@ -63,7 +63,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times.setdefault((v, gm, epi), []).append(e0.elapsed_time(e1) / 5 * 1e-3)
-                if rnd == 0 and (v < 10 or 40 <= v < 50):
+                if rnd == 0 and (v < 10 or 40 <= v < 60):
                     if epi not in ref:
                         ref[epi] = C.clone()
                     else:
