@@ -24,6 +24,13 @@ PIPNET_DEV float wave_max(float v) {
 }
 
 PIPNET_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+// Retire every outstanding vector-memory load with a wait hipcc's wait-count pass can see (an
+// asm waitcnt is opaque to it).  Epilogues call it once, after their bias / residual preloads
+// and before their row-guarded store loop: the pass cannot count stores issued inside
+// `if (m < M)` branches, so without it every use of a preloaded register waited vmcnt(0) --
+// for all the earlier stores of the loop as well (round 4, profiles/r04/epilogue_vmcnt_ab.txt).
+PIPNET_DEV void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0), gfx9 encoding
 PIPNET_DEV void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 
 // exact (erf) GELU, torch nn.GELU(approximate='none')

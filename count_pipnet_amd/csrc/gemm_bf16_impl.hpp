@@ -259,6 +259,7 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
 #pragma unroll
       for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * LD + j * 32 + lr] = acc[i][j][v];
     __syncthreads();
+    if (i == 0) vm_drain();                      // bias / residual preloads landed (common.hpp)
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int row = it * RPI + lane / CPR;
@@ -535,6 +536,7 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
         for (int i = 0; i < 4; ++i)
           wt[(r * 16 + 4 * (lane >> 4) + i) * EPI_LD + nn * 16 + fr] = acc[half * 4 + r][nn][i];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (half == 0) vm_drain();                   // bias / residual preloads landed (common.hpp)
 #pragma unroll
     for (int it = 0; it < 2 * nr; ++it) {
       const int row = it * 8 + (lane >> 3);
@@ -1455,6 +1457,7 @@ __global__ __launch_bounds__(hsm::NT, 2) void conv3x3_bf16_hsmall_kernel(ConvPar
 #pragma unroll
       for (int v = 0; v < 16; ++v) wt[((v & 3) + 8 * (v >> 2) + 4 * lh) * EPI_LD + 32 * j + lr] = acc[i][j][v];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (i == 0) vm_drain();                      // bias preloads landed (common.hpp)
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int row = 8 * it + (lane >> 3);

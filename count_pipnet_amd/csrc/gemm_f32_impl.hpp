@@ -384,15 +384,26 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
     slab_write(wt, acc, i, lane);
     __syncthreads();
     lab_stamp<ABL>(p, 8 + 2 * i);
+    if (i == 0) vm_drain();               // bias / residual preloads landed (common.hpp)
+    // the slab's 8 LDS reads issued together, outside the row-guarded stores (one latency)
+    f32x4 sv[8];
+#pragma unroll
+    for (int it = 0; it < 8; ++it) sv[it] = ld4(wt + (it * 4 + (lane >> 4)) * 64 + 4 * c4);
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int row = it * 4 + (lane >> 4);
       const int m = m0 + wm * 32 * TM + i * 32 + row;
       float rs = 1.f;
       if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
-      const f32x4 x = epi_math<EPI>(ld4(wt + row * 64 + 4 * c4), bn, sn, HAS_R ? r[i][it] : bn, rs);
+      const f32x4 x = epi_math<EPI>(sv[it], bn, sn, HAS_R ? r[i][it] : bn, rs);
       if (m < p.M && nok) st4_c(op, x, p.plain_store);
       op += 4 * p.ldc;
+      if constexpr ((ABL & 8) != 0) {     // lab: per-iteration timing of the first slab
+        if (i == 0 && it == 0) lab_stamp<ABL>(p, 12);
+        if (i == 0 && it == 1) lab_stamp<ABL>(p, 13);
+        if (i == 0 && it == 3) lab_stamp<ABL>(p, 14);
+        if (i == 0 && it == 5) lab_stamp<ABL>(p, 15);
+      }
     }
     lab_stamp<ABL>(p, 9 + 2 * i);
   }

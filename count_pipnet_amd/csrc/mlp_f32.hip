@@ -214,18 +214,28 @@ __global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __res
 #pragma unroll
       for (int cb = 0; cb < C / 16; ++cb) acc[u][cb] = acc[u][cb] + ld4(ex + (u * (C / 16) + cb) * 4);
   }
-  // ---- epilogue: x[pixel][c .. c+3] += gamma * (acc + b2), c = 16 cb + 4 q ----
+  // ---- epilogue: x[pixel][c .. c+3] += gamma * (acc + b2), c = 16 cb + 4 q.  Every load (x rows
+  // clamped to M - 1) is issued, and retired by one vm_drain, before the first store: loads
+  // issued between row-guarded stores made hipcc wait vmcnt(0) -- for the stores too -- per chunk ----
 #pragma unroll
   for (int u = 0; u < PX; ++u) {
     const int pix = pix0 + 16 * u;
+    const float* xs = x + (int64_t)(pix < M ? pix : M - 1) * C;
+    f32x4 r[C / 16], bb[C / 16], gm[C / 16];
+#pragma unroll
+    for (int cb = 0; cb < C / 16; ++cb) {
+      const int c = 16 * cb + 4 * q;
+      r[cb] = ld4(xs + c);
+      bb[cb] = ld4(b2 + c);
+      gm[cb] = ld4(gamma + c);
+    }
+    vm_drain();
     if (pix < M) {
       float* xr = x + (int64_t)pix * C;
 #pragma unroll
       for (int cb = 0; cb < C / 16; ++cb) {
         const int c = 16 * cb + 4 * q;
-        const f32x4 r = ld4(xr + c);
-        const f32x4 bb = ld4(b2 + c), gm = ld4(gamma + c);
-        st4(xr + c, r + gm * (acc[u][cb] + bb));
+        st4(xr + c, r[cb] + gm[cb] * (acc[u][cb] + bb[cb]));
       }
     }
   }

@@ -95,6 +95,11 @@ def main():
                 names += ["to end"]
             print("   epilogue median cycles: " + "  ".join(f"{nm} {np.median(v):.0f}" for nm, v in zip(names, ph)),
                   flush=True)
+            if (a[:, 12] > 0).all() and (a[:, 15] > 0).all():   # first slab, per store iteration
+                it = [a[:, 12] - a[:, 8], a[:, 13] - a[:, 12], a[:, 14] - a[:, 13], a[:, 15] - a[:, 14],
+                      a[:, 9] - a[:, 15]]
+                print("   first slab median cycles: it0 {:.0f}  it1 {:.0f}  it2-3 {:.0f}  it4-5 {:.0f}  it6-7 {:.0f}".format(
+                    *[np.median(v) for v in it]), flush=True)
         share = (pro.sum(), main_.sum(), epi_.sum())
         tot = sum(share)
         print(f"   wg-time share: prologue {share[0] / tot:.3f} main {share[1] / tot:.3f} epilogue {share[2] / tot:.3f}"
