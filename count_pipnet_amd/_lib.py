@@ -25,14 +25,7 @@ SIGNATURES = {
     "pipnet_amd_abi_version": [],
     "pipnet_amd_status_string": [I32],
     "pipnet_amd_source_digest": [],
-    "pipnet_gemm_persist": [I32],
-    "pipnet_gemm_stream": [I32],
-    "pipnet_conv_bf16_rb": [I32],
-    "pipnet_gemm_bk16x3": [I32],
-    "pipnet_gemm_plain_store": [I32],
-    "pipnet_head_bf16_quads": [I32],
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
-    "pipnet_linear_agelu_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],
     "pipnet_linear_splitk_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, I32, P, P],
     "pipnet_matmul_f64acc_f32": [P, I64, P, I64, P, I64, I32, I32, I32, P],
@@ -65,6 +58,8 @@ SIGNATURES = {
     "pipnet_dwconv7_ln_f32": [P, I32, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_layernorm_f32": [P, I64, I32, P, P, P, P],
     "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],
+    "pipnet_softmax_pool_linear_f32": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P],
+    "pipnet_softmax_pool_linear_bf16": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P],
     "pipnet_nonneg_linear_f32": [P, I32, I32, P, P, I32, I32, F32, P, P, P],
     "pipnet_count_gumbel_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_count_gumbel_devseed_f32": [P, I32, I32, I32, F32, P, P, P, P],
@@ -111,7 +106,7 @@ EPI_GELU_BWD = 8
 EPI_S3_GELU, EPI_F32_BIAS, EPI_F32_RESID = 9, 10, 11      # split-bf16 ("bf16x3") ConvNeXt path
 EPI_DUAL_BIAS_RELU = 12        # pipnet_conv1x1_bf16_dual: downsample + conv1 of a first Bottleneck
 
-ABI_VERSION = 2          # include/pipnet_amd.h PIPNET_AMD_ABI_VERSION
+ABI_VERSION = 3          # include/pipnet_amd.h PIPNET_AMD_ABI_VERSION
 
 _lib = None
 

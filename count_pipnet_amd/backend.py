@@ -65,12 +65,27 @@ def invalidate_weight_caches(net: torch.nn.Module) -> int:
     return n
 
 
-def packed_ready() -> None:
-    """Call right after a weight cache was (re)built: the repacking kernels ran on the current
-    stream, and a concurrent sub-batch forward on another HIP stream (pipnet.set_stream_split)
-    would read the new buffers without waiting for them.  Host-synchronises the current stream
-    on a cache miss only (first forward, or after a weight change), never during graph capture
-    (captures replay warm caches)."""
-    if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
-        torch.cuda.current_stream().synchronize()
+_CROSS = threading.local()
 
+
+@contextlib.contextmanager
+def cross_stream_forward():
+    """Marks a forward whose sub-batches run on several HIP streams (the split forwards of
+    pipnet.py / count_pipnet.py): a weight cache rebuilt inside it is read by the other streams."""
+    _CROSS.depth = getattr(_CROSS, "depth", 0) + 1
+    try:
+        yield
+    finally:
+        _CROSS.depth -= 1
+
+
+def packed_ready() -> None:
+    """Call right after a weight cache was (re)built.  Inside ``cross_stream_forward`` the
+    repacking kernels ran on one sub-batch stream and the other streams would read the new
+    buffers without waiting for them, so the current stream is host-synchronised there -- on a
+    cache miss only (first forward, or after a weight change), never during graph capture
+    (captures replay warm caches).  Everywhere else (one-stream forwards, the training steps,
+    whose trainable weights change every step) the rebuilt buffer is stream-ordered before its
+    readers already and nothing waits."""
+    if getattr(_CROSS, "depth", 0) and torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream().synchronize()

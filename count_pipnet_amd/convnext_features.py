@@ -246,11 +246,10 @@ def packed(cache: Dict, key: str, t: Tensor, fn) -> Tensor:
 
 
 FUSED_MLP = True      # tools / A-B runs may switch the fused narrow-stage MLP off
-# CNBlock GELU applied on Linear2's A-load (pipnet_linear_agelu_f32) rather than in Linear1's
-# epilogue: bitwise the same outputs, but C2 22.06 -> 24.31 ms per step (tools/ab_toggle.py
-# count_pipnet_amd.convnext_features.DEFER_GELU c2, profiles/r04/ab_c2_defer_gelu.txt): the
-# packed GELU VALU between Linear2's MFMAs stalls them more than Linear1's epilogue did.  Off.
-DEFER_GELU = False
+# (Round 4 measured the CNBlock GELU applied on Linear2's A-load instead of in Linear1's
+# epilogue: bitwise the same outputs, C2 22.06 -> 24.31 ms per step, profiles/r04/
+# ab_c2_defer_gelu.txt -- the packed GELU VALU between Linear2's MFMAs stalls them more than the
+# epilogue does.  Removed from the library in round 5.)
 # The fused MLP parallelises over pixels only (16 per wave): on small feature maps (C1's 64^2
 # inputs: 256 / 64 pixels per image) the unfused GEMMs, which also spread the hidden dimension
 # over workgroups, are faster.  The choice depends on the layer's C and h*w, never on the batch
@@ -278,13 +277,6 @@ def _cnblock_hip(blk: CNBlock, h: Tensor, cache: Dict, key: str, row_scale: Opti
         K.cnblock_mlp(t.view(-1, c), l1.weight, l1.bias, l2.weight, l2.bias, blk.layer_scale.view(-1), hv, hw=hh * ww)
         return h
     m, hid = hv.shape[0], l1.weight.shape[0]
-    if row_scale is None and DEFER_GELU and K.linear_agelu_ok(m, c, hid):
-        # GELU on Linear2's A-load instead of in Linear1's epilogue: bitwise the same values, the
-        # GELU VALU work issued between Linear2's MFMAs (the epilogue form held stage-3 Linear1
-        # 7 % below its bias-only rate, profiles/r04/)
-        u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS)
-        K.linear_agelu(u, l2.weight, l2.bias, _lib.EPI_RESID, scale=blk.layer_scale.view(-1), r=hv, out=hv)
-        return h
     u = K.linear(t.view(-1, c), l1.weight, l1.bias, _lib.EPI_BIAS_GELU)
     if row_scale is None:
         K.linear(u, l2.weight, l2.bias, _lib.EPI_RESID, scale=blk.layer_scale.view(-1), r=hv, out=hv)

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from . import kernels as K
-from .backend import packed_ready, use_hip
+from .backend import cross_stream_forward, packed_ready, use_hip
 from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
 from .count_pipnet_utils import (BilinearIntermediate, ClampSTE, GumbelSoftmax, IdentityIntermediate,
                                  LinearFull, LinearIntermediate, OneHotEncoder, STE_Round)
@@ -71,7 +71,8 @@ class CountPIPNet(nn.Module):
         n = stream_split(self, xs)
         # (the Philox offset of a sub-batch, b0*h*w*P/4 blocks, is exact for P % 4 == 0)
         if n > 1 and self._num_prototypes % 4 == 0 and not torch.cuda.is_current_stream_capturing():
-            return self._forward_hip_split(xs, inference, n)
+            with cross_stream_forward():
+                return self._forward_hip_split(xs, inference, n)
         feats = as_nhwc(self._net(xs))
         act = list(self._add_on)[-1] if isinstance(self._add_on, nn.Sequential) else self._add_on
         do_round = bool(self._use_ste or inference)

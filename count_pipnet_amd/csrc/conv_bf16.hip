@@ -1,8 +1,6 @@
 // bf16 ResNet path (BASELINE C3): implicit-GEMM convolution (gemm_bf16_impl.hpp), NCHW fp32
 // -> NHWC bf16 input relayout, NHWC bf16 max-pool.  Reference: features/resnet_features.py
 // (conv / BatchNorm / ReLU / Bottleneck / MaxPool2d, :77-229).
-#include <cstdlib>
-
 #include "gemm_bf16_impl.hpp"
 
 using namespace pipnet_bf16;
@@ -11,18 +9,13 @@ namespace {
 
 int grid_for(int64_t n) { return (int)((n + 255) / 256 < 8192 ? (n + 255) / 256 : 8192); }
 
-// compute units of the current device (one persistent workgroup each), queried once
+// compute units of the current device (one persistent workgroup each), queried per launch
 int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-  }
-  return n;
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      v > 0)
+    return v;
+  return 256;
 }
 
 int choose_group_m(int K) {
@@ -102,41 +95,10 @@ bool halo_ok(const ConvParams& p, int epi) {
 int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
 
 // Row blocks per wave group of the 256-wide ping-pong tiles (halo 8, persistent 9): 8 -> 256-row
-// tiles, 7 -> 224-row tiles.  C3's layers have M = 784 per image, so at 64 images 196 row tiles
-// of 256 leave 60 CUs idle (N = 256) or a half-empty last round (N = 512: 392 tiles = 1.53
-// rounds); 224 rows give 224 / 448 tiles (0.875 / 1.75 rounds).  Cost model: rounds of tiles x
-// tile work, a 224-row tile charged 7/8 of a 256-row one plus 3 % (B is fetched whole for 7/8 of
-// the rows).  Every output element is the same MFMA chain over the same K order in both forms,
-// so this M-dependent choice keeps every pixel's bits batch-invariant.  Mirrored by
-// kernels.py:bf16_pp_rb.  pipnet_conv_bf16_rb (or PIPNET_PP_RB=7/8 in the environment) forces one
-// form, for tests and A/B runs.
-// Modes: 0 = automatic for both tiles, 7 / 8 = forced for both, 1 = automatic for the halo
-// tile only (persistent tile at 256 rows), 2 = automatic for the persistent tile only.
-// Default 8: C3 runs its batch as two concurrent half-batch streams, which already fill the CUs a
-// short last round leaves idle, and there the 256-row tiles' better bytes-per-MFMA wins -- C3
-// end to end 6.00 (8) vs 6.11 (0) / 6.03 (1) / 6.07 (2) ms; with ONE stream the automatic
-// choice wins, 6.62 vs 6.78 ms (profiles/r04/ab_c3_rb224.txt).
-int g_pp_rb = -1;
-bool rb_mode_ok(int v) { return v == 0 || v == 1 || v == 2 || v == 7 || v == 8; }
-int pp_rb_mode() {
-  if (g_pp_rb < 0) {
-    const char* e = getenv("PIPNET_PP_RB");
-    const int v = e ? atoi(e) : 8;
-    g_pp_rb = rb_mode_ok(v) ? v : 8;
-  }
-  return g_pp_rb;
-}
-int pick_rb(int M, int nt, bool halo) {
-  const int mode = pp_rb_mode();
-  if (mode == 7 || mode == 8) return mode;
-  if ((mode == 1 && !halo) || (mode == 2 && halo)) return 8;
-  const int64_t ncu = num_cus();
-  auto cost = [&](int rb) {
-    const int64_t tiles = (int64_t)((M + 32 * rb - 1) / (32 * rb)) * nt;
-    return (double)((tiles + ncu - 1) / ncu) * (rb == 8 ? 1.0 : 0.875 * 1.03);
-  };
-  return cost(7) < cost(8) ? 7 : 8;
-}
+// tiles.  (224-row tiles, RB = 7, gave the single-stream C3 +2 % on the layers whose 256-row grid
+// leaves a short last round, but lost under the two-stream default, which already fills those
+// rounds: 6.00 vs 6.11 ms, profiles/r04/ab_c3_rb224.txt; the template keeps RB for the lab.)
+constexpr int PP_RB = 8;
 
 template <int ALOAD>
 int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
@@ -180,15 +142,13 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   }
   if (v == 9) {                                  // persistent 256 x 256 ping-pong (1x1, N % 256 == 0)
     p.nt = p.N / 256;
-    const int rb = pick_rb(p.M, p.nt, false);
-    p.mt = (p.M + 32 * rb - 1) / (32 * rb);
+    p.mt = (p.M + 32 * PP_RB - 1) / (32 * PP_RB);
     p.group_m = choose_group_m(p.K);
     const int ntiles = p.mt * p.nt;
     const dim3 grid(ntiles < num_cus() ? ntiles : num_cus());
 #define PIPNET_PPP(E)                                                                                  \
   case E:                                                                                               \
-    if (rb == 7) hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 7>), grid, dim3(512), 0, s, p);           \
-    else hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, 8>), grid, dim3(512), 0, s, p);                   \
+    hipLaunchKernelGGL((conv_bf16_ppp_kernel<E, PP_RB>), grid, dim3(512), 0, s, p);                   \
     break;
     switch (epi) {
       PIPNET_PPP(PIPNET_EPI_NONE)
@@ -206,14 +166,12 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
   if (v == 8) {                                  // ping-pong with the LDS input halo, 256 x 64 NB
     const int nb = halo_nb(p.N);
     p.nt = (p.N + 64 * nb - 1) / (64 * nb);
-    const int rb = nb == 4 ? pick_rb(p.M, p.nt, true) : 8;
-    p.mt = (p.M + 32 * rb - 1) / (32 * rb);
+    p.mt = (p.M + 32 * PP_RB - 1) / (32 * PP_RB);
     p.group_m = choose_group_m(p.K);
     const dim3 grid(p.mt * p.nt);
 #define PIPNET_HALO(E)                                                                                \
   case E:                                                                                              \
-    if (nb == 4 && rb == 7) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4, 7>), grid, dim3(512), 0, s, p); \
-    else if (nb == 4) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4, 8>), grid, dim3(512), 0, s, p); \
+    if (nb == 4) hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<E, 4, PP_RB>), grid, dim3(512), 0, s, p); \
     else return PIPNET_ERR_ARG;                                                                        \
     break;
     switch (epi) {
@@ -439,12 +397,6 @@ extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int C
                                        const void* R, int epilogue, void* y, void* stream) {
   return pipnet_conv2d_nhwc_bf16_tile(x, B, H, W, Cin, w_packed, bias, Cout, KH, KW, stride, pad, R, epilogue, y, -1,
                                       stream);
-}
-
-extern "C" int pipnet_conv_bf16_rb(int mode) {
-  if (rb_mode_ok(mode)) g_pp_rb = mode;
-  else if (mode != -1) return -PIPNET_ERR_ARG;
-  return pp_rb_mode();
 }
 
 extern "C" int pipnet_conv1x1_bf16_dual(const void* x, int64_t M, int Cin, const void* w_packed, const float* bias,

@@ -55,7 +55,7 @@ enum { ALOAD_DENSE = 0, ALOAD_CONV = 2 };
 // virtual split-plane channel -> physical (K-tiles never straddle a segment: seg % 32 == 0)
 PIPNET_DEV int seg_remap(const ConvParams& p, int c) { return (p.seg && c >= 2 * p.seg) ? c - 2 * p.seg : c; }
 
-static __device__ __attribute__((aligned(16))) float g_zero_bf[4] = {0.f, 0.f, 0.f, 0.f};
+static __device__ const __attribute__((aligned(16))) float g_zero_bf[4] = {0.f, 0.f, 0.f, 0.f};
 
 struct ARow {
   int64_t base;

@@ -1,12 +1,6 @@
 // Product instantiation of the fp32 MFMA GEMM (templates + design notes: gemm_f32_impl.hpp).
 #include "gemm_f32_impl.hpp"
 
-#include <cstdlib>
-
-#ifndef PIPNET_GEMM_PERSIST_DEFAULT
-#define PIPNET_GEMM_PERSIST_DEFAULT 0
-#endif
-
 using namespace pipnet_gemm;
 
 namespace {
@@ -57,74 +51,14 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
-// compute units of the current device, queried once
+// compute units of the current device (queried per launch: no process-wide cache, so every
+// device of a multi-GPU process gets its own answer; the runtime serves it from its device table)
 int num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
-  }
-  return n;
-}
-
-// PIPNET_GEMM_PERSIST=0/1 (read once): the persistent 128x128 tile for variant-3 dense GEMMs
-// with N % 128 == 0 (A/B switch; the default is set from tools/gemm_bench.py runs).
-int g_gemm_persist = -1;
-bool gemm_persist() {
-  if (g_gemm_persist < 0) {
-    const char* e = getenv("PIPNET_GEMM_PERSIST");
-    g_gemm_persist = e ? (e[0] == '1') : PIPNET_GEMM_PERSIST_DEFAULT;
-  }
-  return g_gemm_persist == 1;
-}
-
-// PIPNET_GEMM_STREAM=0/1 (read once; default 0 -- measured 3-5 % slower than the regular tile, profiles/r03/gemm_stream_ab.txt): the streaming persistent tile with deferred
-// epilogues (gemm_f32_tn_stream_kernel) for variant-3 dense GEMMs with N % 128 == 0, K >= 256
-// and at least two tiles per workgroup slot.
-#ifndef PIPNET_GEMM_STREAM_DEFAULT
-#define PIPNET_GEMM_STREAM_DEFAULT 0
-#endif
-int g_gemm_stream = -1;
-bool gemm_stream() {
-  if (g_gemm_stream < 0) {
-    const char* e = getenv("PIPNET_GEMM_STREAM");
-    g_gemm_stream = e ? (e[0] == '1') : PIPNET_GEMM_STREAM_DEFAULT;
-  }
-  return g_gemm_stream == 1;
-}
-
-// PIPNET_GEMM_BK16X3=0/1 (read once; pipnet_gemm_bk16x3): the 128-row tile with 16-deep K-tiles
-// in 2 LDS stages (32 KiB) at 3 workgroups per CU for the short-K, wide-N GEMMs (stage-3 fc1: N
-// 1536, K 384): while one workgroup runs its GELU epilogue two others keep every SIMD's MFMA
-// pipe fed (2 workgroups per CU leave one wave per SIMD).  tools/gemm_lab.py v8 vs v0:
-// s384_fc1 111.6 vs 106.3 TF, but the K >= 768 shapes lose (profiles/r04/gemm_lab_3wg.log).
-#ifndef PIPNET_GEMM_BK16X3_DEFAULT
-#define PIPNET_GEMM_BK16X3_DEFAULT 0
-#endif
-int g_gemm_bk16x3 = -1;
-bool gemm_bk16x3() {
-  if (g_gemm_bk16x3 < 0) {
-    const char* e = getenv("PIPNET_GEMM_BK16X3");
-    g_gemm_bk16x3 = e ? (e[0] == '1') : PIPNET_GEMM_BK16X3_DEFAULT;
-  }
-  return g_gemm_bk16x3 == 1;
-}
-// Output-tile store policy of the GEMMs launched through launch_gemm: 0 = non-temporal (default),
-// 1 = plain.  pipnet_gemm_plain_store or PIPNET_GEMM_PLAIN_STORE=1 switch it.
-int g_gemm_plain = -1;
-int gemm_plain_store() {
-  if (g_gemm_plain < 0) {
-    const char* e = getenv("PIPNET_GEMM_PLAIN_STORE");
-    g_gemm_plain = e ? (e[0] == '1') : 0;
-  }
-  return g_gemm_plain;
-}
-bool bk16x3_shape(const GemmParams& p) {
-  return p.N % 128 == 0 && p.N >= 1024 && p.K % 16 == 0 && p.K >= 256 && p.K <= 512 && p.M > 64;
+  int dev = 0, v = 0;
+  if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      v > 0)
+    return v;
+  return 256;
 }
 
 template <int ALOAD>
@@ -135,58 +69,12 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
-  p.plain_store = gemm_plain_store();
-  int v = gemm_variant(p.M, p.N, p.K, vec);
-  if (v == 3 && epi != PIPNET_EPI_RESID_ROWSCALE && bk16x3_shape(p) && gemm_bk16x3()) v = 4;
+  const int v = gemm_variant(p.M, p.N, p.K, vec);
   p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
   const dim3 grid(p.mt * p.nt), block(NTHREADS);
-  if (ALOAD == ALOAD_DENSE && v == 3 && p.vec_epi && p.N % BN == 0 && p.K % 32 == 0 && p.K >= 256 &&
-      epi != PIPNET_EPI_RESID_ROWSCALE && p.mt * p.nt >= 4 * num_cus() && (int64_t)p.M * p.lda < (1LL << 31) &&
-      (int64_t)p.N * p.K < (1LL << 31) && (int64_t)p.M * p.ldc < (1LL << 31) &&
-      (!p.R || (int64_t)p.M * p.ldr < (1LL << 31)) && gemm_stream()) {
-    const dim3 sgrid(2 * num_cus());
-#define PIPNET_STREAM_CASE(E) \
-  case E: hipLaunchKernelGGL((gemm_f32_tn_stream_kernel<E>), sgrid, block, 0, s, p); break;
-    switch (epi) {
-      PIPNET_STREAM_CASE(PIPNET_EPI_NONE)
-      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS)
-      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_GELU)
-      PIPNET_STREAM_CASE(PIPNET_EPI_RESID)
-      PIPNET_STREAM_CASE(PIPNET_EPI_MUL)
-      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_RELU)
-      PIPNET_STREAM_CASE(PIPNET_EPI_BIAS_RESID_RELU)
-      PIPNET_STREAM_CASE(PIPNET_EPI_GELU_BWD)
-      default: return PIPNET_ERR_ARG;
-    }
-#undef PIPNET_STREAM_CASE
-    PIPNET_CHECK_LAUNCH();
-    return PIPNET_OK;
-  }
-  if (ALOAD == ALOAD_DENSE && v == 3 && p.vec_epi && p.N % BN == 0 && gemm_persist()) {
-    const int ntiles = p.mt * p.nt;
-    const dim3 pgrid(ntiles < 2 * num_cus() ? ntiles : 2 * num_cus());
-#define PIPNET_PERSIST_CASE(E) \
-  case E: hipLaunchKernelGGL((gemm_f32_tn_persist_kernel<E>), pgrid, block, 0, s, p); break;
-    switch (epi) {
-      PIPNET_PERSIST_CASE(PIPNET_EPI_NONE)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_GELU)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_RESID)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_MUL)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_RELU)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_BIAS_RESID_RELU)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_RESID_ROWSCALE)
-      PIPNET_PERSIST_CASE(PIPNET_EPI_GELU_BWD)
-      default: return PIPNET_ERR_ARG;
-    }
-#undef PIPNET_PERSIST_CASE
-    PIPNET_CHECK_LAUNCH();
-    return PIPNET_OK;
-  }
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
     if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
-    else if (v == 4) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 3, 2>), grid, block, 0, s, p); \
     else if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2, 0, true>), grid, \
                                                    block, 0, s, p);                                         \
     else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2>), grid, block, 0, s, p); \
@@ -212,30 +100,6 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
 
 }  // namespace
 
-extern "C" int pipnet_gemm_persist(int mode) {
-  if (mode == 0 || mode == 1) g_gemm_persist = mode;
-  else if (mode != -1) return PIPNET_ERR_ARG;
-  return gemm_persist() ? 1 : 0;
-}
-
-extern "C" int pipnet_gemm_plain_store(int mode) {
-  if (mode == 0 || mode == 1) g_gemm_plain = mode;
-  else if (mode != -1) return PIPNET_ERR_ARG;
-  return gemm_plain_store();
-}
-
-extern "C" int pipnet_gemm_bk16x3(int mode) {
-  if (mode == 0 || mode == 1) g_gemm_bk16x3 = mode;
-  else if (mode != -1) return PIPNET_ERR_ARG;
-  return gemm_bk16x3() ? 1 : 0;
-}
-
-extern "C" int pipnet_gemm_stream(int mode) {
-  if (mode == 0 || mode == 1) g_gemm_stream = mode;
-  else if (mode != -1) return PIPNET_ERR_ARG;
-  return gemm_stream() ? 1 : 0;
-}
-
 extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
                                  const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                                  int M, int N, int K, int epilogue, void* stream) {
@@ -254,49 +118,6 @@ extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, co
   p.A = A; p.lda = lda; p.W = W; p.bias = bias; p.scale = scale; p.R = R; p.ldr = ldr;
   p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
   return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
-}
-
-// GELU on A-load (the deferred CNBlock GELU): C = epi(gelu_erf(A) W^T) on the BK-32 tiles of
-// variants 2 / 3 (64- or 128-row), for dense A only.  The CNBlock runs Linear1 with EPI_BIAS and
-// this Linear2 applies the GELU to each A fragment in registers: bitwise the EPI_BIAS_GELU +
-// plain-Linear2 path (same gelu_pk16 of the same fp32 value), with the GELU VALU work issued
-// between Linear2's MFMAs instead of in a Linear1 epilogue that holds the MFMA pipe idle
-// (tools/gemm_lab.py: the GELU epilogue costs the stage-3 Linear1 7 %, profiles/r04/).
-template <int E>
-int launch_agelu(GemmParams& p, int v, hipStream_t s) {
-  p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
-  const dim3 grid(p.mt * p.nt), block(NTHREADS);
-  if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD_DENSE, 3, 2, 0, true, true>), grid, block, 0, s, p);
-  else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD_DENSE, 3, 2, 0, false, true>), grid, block, 0, s, p);
-  else hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 2, E, ALOAD_DENSE, 2, 2, 0, false, true>), grid, block, 0, s, p);
-  PIPNET_CHECK_LAUNCH();
-  return PIPNET_OK;
-}
-
-extern "C" int pipnet_linear_agelu_f32(const float* A, int64_t lda, const float* W, const float* bias,
-                                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
-                                       int M, int N, int K, int epilogue, void* stream) {
-  if (M < 0 || N < 0 || K <= 0) return PIPNET_ERR_ARG;
-  if (M == 0 || N == 0) return PIPNET_OK;
-  if (epilogue != PIPNET_EPI_NONE && epilogue != PIPNET_EPI_BIAS && epilogue != PIPNET_EPI_RESID) return PIPNET_ERR_ARG;
-  if ((K & 31) || (lda & 3) || lda < K || ldc < N || (N & 3) || (ldc & 3)) return PIPNET_ERR_ARG;
-  if (!A || !W || !C || (epilogue == PIPNET_EPI_RESID && (!R || ldr < N || (ldr & 3)))) return PIPNET_ERR_ARG;
-  if (!aligned16(A) || !aligned16(W) || !aligned16(C) || (R && !aligned16(R)) || (bias && !aligned16(bias)) ||
-      (scale && !aligned16(scale)))
-    return PIPNET_ERR_ALIGN;
-  GemmParams p{};
-  p.A = A; p.lda = lda; p.W = W; p.bias = bias; p.scale = scale; p.R = R; p.ldr = ldr;
-  p.C = C; p.ldc = ldc; p.M = M; p.N = N; p.K = K;
-  p.nt = (p.N + BN - 1) / BN;
-  p.group_m = choose_group_m(p);
-  p.vec_epi = 1;
-  const int v = gemm_variant(M, N, K, true);
-  if (v != 2 && v != 3) return PIPNET_ERR_ARG;   // the BK-16 / K-tail tiles have no A-load GELU
-  switch (epilogue) {
-    case PIPNET_EPI_NONE: return launch_agelu<PIPNET_EPI_NONE>(p, v, (hipStream_t)stream);
-    case PIPNET_EPI_BIAS: return launch_agelu<PIPNET_EPI_BIAS>(p, v, (hipStream_t)stream);
-    default: return launch_agelu<PIPNET_EPI_RESID>(p, v, (hipStream_t)stream);
-  }
 }
 
 extern "C" int pipnet_linear_rowscale_f32(const float* A, int64_t lda, const float* W, const float* bias,

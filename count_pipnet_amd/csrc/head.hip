@@ -7,20 +7,27 @@
 //   * count_encode   OneHotEncoder / LinearIntermediate forwards            -- count_pipnet_utils.py
 // One wave owns one patch: lane l holds channels l, l+64, ... so every HBM access is a
 // coalesced 256-B row segment, and the per-patch reductions are 64-lane butterflies.
+#include <type_traits>
+
 #include "common.hpp"
-#include <cstdlib>
 
 namespace {
 // Zero-fill by a kernel rather than a memset call: the launch is captured as an ordinary
 // kernel node when the stream is being recorded into a HIP graph (count_pipnet_amd.graph); a
 // memset issued during capture was observed NOT to take effect on replay.
-__global__ __launch_bounds__(256) void zero_u32_kernel(uint32_t* __restrict__ p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) p[i] = 0u;
+// Two ranges per launch (the fused head zeroes pooled and its arrival tickets together).
+__global__ __launch_bounds__(256) void zero_u32_kernel(uint32_t* __restrict__ p, int64_t n, uint32_t* __restrict__ p2,
+                                                       int64_t n2) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n + n2; i += (int64_t)gridDim.x * 256) {
+    if (i < n) p[i] = 0u;
+    else p2[i - n] = 0u;
+  }
 }
-inline bool zero_fill(void* p, int64_t n_u32, hipStream_t s) {
-  const int64_t blocks = (n_u32 + 255) / 256 < 1024 ? (n_u32 + 255) / 256 : 1024;
+inline bool zero_fill(void* p, int64_t n_u32, hipStream_t s, void* p2 = nullptr, int64_t n2_u32 = 0) {
+  const int64_t n = n_u32 + (p2 ? n2_u32 : 0);
+  const int64_t blocks = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
   hipLaunchKernelGGL(zero_u32_kernel, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, s,
-                     reinterpret_cast<uint32_t*>(p), n_u32);
+                     reinterpret_cast<uint32_t*>(p), n_u32, reinterpret_cast<uint32_t*>(p2), p2 ? n2_u32 : 0);
   return hipGetLastError() == hipSuccess;
 }
 }  // namespace
@@ -31,10 +38,110 @@ constexpr int HEAD_THREADS = 256;
 constexpr int PIX_PER_BLOCK = 32;
 
 // ---------------------------------------------------------------------------------------
-template <int NJ, int MODE, typename T = float>   // MODE 0 = max pool, 1 = sum pool; T = float / __bf16 logits
+// NonNegLinear (pipnet.py:36-37, 54-71) fused into the softmax-pool head: the classifier of
+// image b runs in the LAST workgroup of b's pixel blocks, chosen by an arrival ticket.
+//   * every workgroup's atomicMax of its pixel-block maxima into pooled[b] is acknowledged
+//     (vmcnt(0): a no-return atomic stays counted until performed at the memory side) before
+//     its thread 0 takes a ticket (atomicAdd on tickets[b], also performed there);
+//   * the workgroup that draws gridDim.x - 1 reads pooled[b] back through atomic RMWs
+//     (atomicOr 0: served at the memory side, so no XCD's stale L2 / L1 copy is read),
+//     applies the 0.1 presence threshold in inference mode, writes the clamped row (x_out)
+//     and runs the GEMV x' relu(W)^T + bias against W as it is at call time;
+//   * the GEMV keeps nonneg_linear_kernel's arithmetic exactly (per-thread float4 slices,
+//     16 class partials, fmaf order, wave then cross-wave sums), so the fused head is bitwise
+//     the two-kernel path.
+// Tickets are zeroed by the same zero-fill launch as pooled.
+// ---------------------------------------------------------------------------------------
+constexpr int NN_CLS_PER_BLOCK = 16;
+
+struct HeadLinear {
+  const float* W;        // [K, P] classifier weight (relu applied here, not stored)
+  const float* bias;     // [K] or null
+  int K;
+  int apply_thresh;
+  float thresh;
+  float* x_out;          // [B, P] clamped (or copied) pooled row, or null
+  float* out;            // [B, K] logits
+  int32_t* tickets;      // [B] arrival tickets (zeroed with pooled)
+};
+
+// One row of NonNegLinear: x (P floats, any address space the caller owns) -> out[0..K).
+// Called by all HEAD_THREADS threads of a workgroup; red = [4][16] floats of LDS.
+PIPNET_DEV void nonneg_linear_row(const float* x, int D, const float* __restrict__ W, const float* __restrict__ bias,
+                                  int K, float* __restrict__ outr, float (*red)[NN_CLS_PER_BLOCK]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k0 = 0; k0 < K; k0 += NN_CLS_PER_BLOCK) {
+    const int nk = K - k0 < NN_CLS_PER_BLOCK ? K - k0 : NN_CLS_PER_BLOCK;
+    const float* w0 = W + (int64_t)k0 * D;
+    float s[NN_CLS_PER_BLOCK];
+#pragma unroll
+    for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) s[j] = 0.f;
+    if ((D & 3) == 0) {
+      for (int c = 4 * threadIdx.x; c < D; c += 4 * HEAD_THREADS) {
+        const f32x4 xv = ld4(x + c);
+        // rows past nk load row nk-1 and are discarded: a load under a per-class branch
+        // made the compiler wait for each one (16 serialised round trips per slice)
+#pragma unroll
+        for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
+          const f32x4 w = ld4(w0 + (int64_t)(j < nk ? j : nk - 1) * D + c);
+          s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
+          s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
+          s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
+          s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
+        }
+      }
+    } else {
+      for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
+        const float xv = x[c];
+#pragma unroll
+        for (int j = 0; j < NN_CLS_PER_BLOCK; ++j)
+          s[j] = fmaf(xv, fmaxf(w0[(int64_t)(j < nk ? j : nk - 1) * D + c], 0.f), s[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
+      const float t = wave_sum(s[j]);
+      if (lane == 0) red[wv][j] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < nk) {
+      const int k = k0 + threadIdx.x;
+      float t = red[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < HEAD_THREADS / 64; ++w) t += red[w][threadIdx.x];
+      outr[k] = t + (bias ? bias[k] : 0.f);
+    }
+    __syncthreads();
+  }
+}
+
+// The fused head's tail (after the workgroup's atomicMax loop).  xs = >= P floats of LDS the
+// workgroup no longer needs.
+PIPNET_DEV void head_linear_tail(const HeadLinear& hl, int b, int P, float* pooled, float* xs) {
+  __shared__ int is_last;
+  __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
+  vm_drain();                                  // this thread's atomicMax ops performed
+  __syncthreads();
+  if (threadIdx.x == 0) is_last = atomicAdd(hl.tickets + b, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!is_last) return;
+  unsigned* prow = reinterpret_cast<unsigned*>(pooled + (int64_t)b * P);
+  for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
+    float v = __uint_as_float(atomicOr(prow + c, 0u));
+    if (hl.apply_thresh && v < hl.thresh) v = 0.f;
+    xs[c] = v;
+    if (hl.x_out) hl.x_out[(int64_t)b * P + c] = v;
+  }
+  __syncthreads();
+  nonneg_linear_row(xs, P, hl.W, hl.bias, hl.K, hl.out + (int64_t)b * hl.K, red);
+}
+
+// ---------------------------------------------------------------------------------------
+// MODE 0 = max pool, 1 = sum pool; T = float / __bf16 logits; LIN: + the fused NonNegLinear tail
+template <int NJ, int MODE, typename T = float, bool LIN = false>
 __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __restrict__ feat, int HW, int P,
                                                                     float* __restrict__ proto,
-                                                                    float* __restrict__ pooled) {
+                                                                    float* __restrict__ pooled, HeadLinear hl) {
   __shared__ float red[HEAD_THREADS / 64][NJ * 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int b = blockIdx.y;
@@ -86,115 +193,20 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
     else
       atomicAdd(dst, r);
   }
+  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);
 }
 
-// bf16 logits (the C3 ResNet build, P = 2048): 16-B loads of 8 consecutive channels per
-// lane (vector j of lane l = channels 8l + 512j ..), 2 x 16-B fp32 stores, so one wave
-// instruction moves 1 KiB of logits / 2 KiB of proto (the lane-strided kernel above would
-// issue 2-byte loads here: 1.85 TB/s measured).  P % 8 == 0, P <= 512 NV.
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-
-template <int NV, int MODE>
-__global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16v_kernel(const __bf16* __restrict__ feat, int HW,
-                                                                          int P, float* __restrict__ proto,
-                                                                          float* __restrict__ pooled) {
-  __shared__ float red[HEAD_THREADS / 64][NV * 512];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = blockIdx.y;
-  const int pix0 = blockIdx.x * PIX_PER_BLOCK;
-  float racc[NV][8];
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) racc[j][e] = 0.f;
-  // the next pixel's logits are requested under the current one's math (one HBM latency per
-  // wave per pixel otherwise: the wave walks its pixels serially)
-  constexpr int STEP = HEAD_THREADS / 64;
-  bf16x8_t xc[NV], xn[NV];
-  auto load_pix = [&](int pix, bf16x8_t (&x)[NV]) {
-    const int64_t base = ((int64_t)b * HW + pix) * P;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = 8 * lane + 512 * j;
-      if (c < P) x[j] = *reinterpret_cast<const bf16x8_t*>(feat + base + c);
-    }
-  };
-  if (wv < PIX_PER_BLOCK && pix0 + wv < HW) load_pix(pix0 + wv, xc);
-  for (int pi = wv; pi < PIX_PER_BLOCK; pi += STEP) {
-    const int pix = pix0 + pi;
-    if (pix >= HW) break;
-    if (pi + STEP < PIX_PER_BLOCK && pix + STEP < HW) load_pix(pix + STEP, xn);
-    const int64_t base = ((int64_t)b * HW + pix) * P;
-    float v[NV][8];
-    float m = -INFINITY;
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = 8 * lane + 512 * j;
-      if (c < P) {
-        const bf16x8_t x = xc[j];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[j][e] = (float)x[e], m = fmaxf(m, v[j][e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[j][e] = -INFINITY;
-      }
-    }
-    m = wave_max(m);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < NV; ++j)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[j][e] = 8 * lane + 512 * j < P ? expf(v[j][e] - m) : 0.f;
-        s += v[j][e];
-      }
-    const float inv = 1.0f / wave_sum(s);
-#pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      const int c = 8 * lane + 512 * j;
-      if (c < P) {
-        f32x4 y0, y1;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) y0[e] = v[j][e] * inv, y1[e] = v[j][4 + e] * inv;
-        __builtin_nontemporal_store(y0, reinterpret_cast<f32x4*>(proto + base + c));   // write-once map
-        __builtin_nontemporal_store(y1, reinterpret_cast<f32x4*>(proto + base + c + 4));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          racc[j][e] = MODE == 0 ? fmaxf(racc[j][e], y0[e]) : racc[j][e] + y0[e];
-          racc[j][4 + e] = MODE == 0 ? fmaxf(racc[j][4 + e], y1[e]) : racc[j][4 + e] + y1[e];
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < NV; ++j) xc[j] = xn[j];
-  }
-#pragma unroll
-  for (int j = 0; j < NV; ++j)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[wv][8 * lane + 512 * j + e] = racc[j][e];
-  __syncthreads();
-  for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
-    float r = red[0][c];
-#pragma unroll
-    for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
-    float* dst = pooled + (int64_t)b * P + c;
-    if (MODE == 0)
-      atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
-    else
-      atomicAdd(dst, r);
-  }
-}
-
-// Quad layout (round 4): lane l holds channels 4l + 256q .. +3 (8-B bf16 loads, 512 B contiguous
-// per wave instruction), so each 16-B fp32 proto store instruction writes 1 KiB contiguous -- 8
-// whole 128-B lines -- where the 8-channel layout above writes every line in two halves from
-// two instructions (proto is 2/3 of this kernel's bytes).  Same per-element exp / scale; the
-// per-lane partial sums of the softmax denominator group channels differently, so the last bits
-// of the denominator can differ from the 8-channel layout's.
-template <int NV, int MODE>
+// bf16 logits (the C3 ResNet build, P = 2048), quad layout (round 4): lane l holds channels
+// 4l + 256q .. +3 (8-B bf16 loads, 512 B contiguous per wave instruction), so each 16-B fp32
+// proto store instruction writes 1 KiB contiguous -- 8 whole 128-B lines (an 8-channels-per-lane
+// layout wrote every line in two halves from two instructions: 322 vs 250 us per 128 images,
+// profiles/r04/pmc_summary_c3.txt; proto is 2/3 of this kernel's bytes).  The next pixel's
+// logits are requested under the current one's math (one HBM latency per wave per pixel
+// otherwise).  P % 8 == 0, P <= 512 NV.
+template <int NV, int MODE, bool LIN = false>
 __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const __bf16* __restrict__ feat, int HW,
                                                                           int P, float* __restrict__ proto,
-                                                                          float* __restrict__ pooled) {
+                                                                          float* __restrict__ pooled, HeadLinear hl) {
   typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
   constexpr int NQ = 2 * NV;
   __shared__ float red[HEAD_THREADS / 64][NV * 512];
@@ -273,21 +285,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
     else
       atomicAdd(dst, r);
   }
-}
-
-// bf16 head layout: 1 = quad layout (softmax_pool_bf16q_kernel, default: C3 +0.6 %,
-// profiles/r04/ab_c3_head_quads.txt), 0 = 8-channel layout;
-// pipnet_head_bf16_quads or PIPNET_HEAD_QUADS=0/1 switch it.
-#ifndef PIPNET_HEAD_QUADS_DEFAULT
-#define PIPNET_HEAD_QUADS_DEFAULT 1
-#endif
-static int g_head_quads = -1;
-static int head_quads() {
-  if (g_head_quads < 0) {
-    const char* e = getenv("PIPNET_HEAD_QUADS");
-    g_head_quads = e ? (e[0] == '1') : PIPNET_HEAD_QUADS_DEFAULT;
-  }
-  return g_head_quads;
+  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -297,8 +295,6 @@ static int head_quads() {
 // loads in flight per thread; C2: D = 768, K = 200 -> 13 blocks per image).  Partials are
 // reduced wave-wise then across the 4 waves in a fixed order (batch-invariant).
 // ---------------------------------------------------------------------------------------
-constexpr int NN_CLS_PER_BLOCK = 16;
-
 __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float* __restrict__ x, int D,
                                                                      const float* __restrict__ W,
                                                                      const float* __restrict__ bias, int K,
@@ -619,69 +615,76 @@ int nj_bucket(int P) {
     default: return PIPNET_ERR_ARG; \
   }
 
+// softmax + pool (+ the fused NonNegLinear when hl.W is set: max pool only).  bf16 logits with
+// P % 8 == 0, P <= 2048 and 16-B aligned operands take the quad-layout kernel.
 template <typename T>
-int softmax_pool_launch(const T* feat, int B, int HW, int P, int pool_mode, float* proto, float* pooled,
-                        void* stream) {
-  if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1)) return PIPNET_ERR_ARG;
+int head_launch(const T* feat, int B, int HW, int P, int pool_mode, float* proto, float* pooled, const HeadLinear& hl,
+                void* stream) {
+  const bool lin = hl.W != nullptr;
+  if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1) || (lin && pool_mode != 0)) return PIPNET_ERR_ARG;
   if (!feat || !proto || !pooled) return PIPNET_ERR_ARG;
+  if (lin && (hl.K <= 0 || !hl.out || !hl.tickets)) return PIPNET_ERR_ARG;
+  if (lin && (P & 3) == 0 && !aligned16(hl.W)) return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
   const int nj = nj_bucket(P);
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (!zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
+  if (!zero_fill(pooled, (int64_t)B * P, s, lin ? hl.tickets : nullptr, B)) return PIPNET_ERR_LAUNCH;
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
+  const dim3 block(HEAD_THREADS);
+  constexpr bool BF = std::is_same<T, __bf16>::value;
+  if (BF && P % 8 == 0 && P <= 2048 && aligned16(feat) && aligned16(proto)) {
+    const __bf16* f = reinterpret_cast<const __bf16*>(feat);
+#define SPQ_CALL(N)                                                                                      \
+    if (lin) hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 0, true>), grid, block, 0, s, f, HW, P, proto, pooled, hl); \
+    else if (pool_mode == 0) hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 0>), grid, block, 0, s, f, HW, P, proto, pooled, hl); \
+    else hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 1>), grid, block, 0, s, f, HW, P, proto, pooled, hl);
+    if (P <= 512) {
+      SPQ_CALL(1)
+    } else if (P <= 1024) {
+      SPQ_CALL(2)
+    } else {
+      SPQ_CALL(4)
+    }
+#undef SPQ_CALL
+  } else {
 #define SP_CALL(N)                                                                                          \
-  if (pool_mode == 0)                                                                                       \
-    hipLaunchKernelGGL((softmax_pool_kernel<N, 0, T>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled); \
-  else                                                                                                      \
-    hipLaunchKernelGGL((softmax_pool_kernel<N, 1, T>), grid, dim3(HEAD_THREADS), 0, s, feat, HW, P, proto, pooled);
-  PIPNET_NJ_SWITCH(nj, SP_CALL)
+    if (lin) hipLaunchKernelGGL((softmax_pool_kernel<N, 0, T, true>), grid, block, 0, s, feat, HW, P, proto, pooled, hl); \
+    else if (pool_mode == 0) hipLaunchKernelGGL((softmax_pool_kernel<N, 0, T>), grid, block, 0, s, feat, HW, P, proto, pooled, hl); \
+    else hipLaunchKernelGGL((softmax_pool_kernel<N, 1, T>), grid, block, 0, s, feat, HW, P, proto, pooled, hl);
+    PIPNET_NJ_SWITCH(nj, SP_CALL)
 #undef SP_CALL
+  }
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
 }
 
 extern "C" int pipnet_softmax_pool_f32(const float* feat, int B, int HW, int P, int pool_mode, float* proto,
                                        float* pooled, void* stream) {
-  return softmax_pool_launch(feat, B, HW, P, pool_mode, proto, pooled, stream);
+  return head_launch(feat, B, HW, P, pool_mode, proto, pooled, HeadLinear{}, stream);
 }
 
 extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
                                         float* pooled, void* stream) {
-  const __bf16* f = reinterpret_cast<const __bf16*>(feat);
-  if (P % 8 || P > 2048 || !aligned16(feat) || !aligned16(proto))
-    return softmax_pool_launch(f, B, HW, P, pool_mode, proto, pooled, stream);
-  if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1) || !pooled) return PIPNET_ERR_ARG;
-  if (B == 0) return PIPNET_OK;
-  hipStream_t s = (hipStream_t)stream;
-  if (!zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;
-  const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
-  const bool quads = head_quads() && P % 4 == 0;
-#define SPV_CALL(N)                                                                                            \
-  if (quads && pool_mode == 0)                                                                                 \
-    hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
-  else if (quads)                                                                                              \
-    hipLaunchKernelGGL((softmax_pool_bf16q_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
-  else if (pool_mode == 0)                                                                                     \
-    hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 0>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled); \
-  else                                                                                                         \
-    hipLaunchKernelGGL((softmax_pool_bf16v_kernel<N, 1>), grid, dim3(HEAD_THREADS), 0, s, f, HW, P, proto, pooled);
-  if (P <= 512) {
-    SPV_CALL(1)
-  } else if (P <= 1024) {
-    SPV_CALL(2)
-  } else {
-    SPV_CALL(4)
-  }
-#undef SPV_CALL
-  PIPNET_CHECK_LAUNCH();
-  return PIPNET_OK;
+  return head_launch(reinterpret_cast<const __bf16*>(feat), B, HW, P, pool_mode, proto, pooled, HeadLinear{}, stream);
 }
 
-extern "C" int pipnet_head_bf16_quads(int mode) {
-  if (mode == 0 || mode == 1) g_head_quads = mode;
-  else if (mode != -1) return PIPNET_ERR_ARG;
-  return head_quads();
+extern "C" int pipnet_softmax_pool_linear_f32(const float* feat, int B, int HW, int P, float* proto, float* pooled,
+                                              const float* W, const float* bias, int K, int apply_thresh,
+                                              float thresh, float* x_out, float* out, int32_t* tickets,
+                                              void* stream) {
+  if (!W) return PIPNET_ERR_ARG;
+  return head_launch(feat, B, HW, P, 0, proto, pooled, HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets},
+                     stream);
+}
+
+extern "C" int pipnet_softmax_pool_linear_bf16(const void* feat, int B, int HW, int P, float* proto, float* pooled,
+                                               const float* W, const float* bias, int K, int apply_thresh,
+                                               float thresh, float* x_out, float* out, int32_t* tickets,
+                                               void* stream) {
+  if (!W) return PIPNET_ERR_ARG;
+  return head_launch(reinterpret_cast<const __bf16*>(feat), B, HW, P, 0, proto, pooled,
+                     HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets}, stream);
 }
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,

@@ -74,15 +74,21 @@ def gather_rows_to_root(x: Tensor, sizes: List[int], group=None, root: int = 0) 
 
 
 def all_gather_rows(x: Tensor, sizes: List[int], group=None) -> Tensor:
-    """Concatenate every rank's ``x`` (rank r holds ``sizes[r]`` rows) on every rank.
-    Uneven shards are padded to the largest one for the collective and trimmed after."""
+    """Concatenate every rank's ``x`` (rank r holds ``sizes[r]`` rows) on every rank: ONE
+    ``all_gather_into_tensor`` straight into the [world * max(sizes), ...] output (no per-rank
+    buffers, no concatenation).  Even shards (the bench and DataParallel's usual case) return
+    that output as is; an uneven shard is padded for the collective and the padding rows are
+    dropped by one compaction copy."""
     world = len(sizes)
     if world == 1:
         return x
-    x = _pad_rows(x, max(sizes))
-    bufs = [torch.empty_like(x) for _ in range(world)]
-    dist.all_gather(bufs, x, group=group)
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+    mx = max(sizes)
+    x = _pad_rows(x, mx)
+    out = torch.empty((world * mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, x, group=group)
+    if all(s == mx for s in sizes):
+        return out
+    return torch.cat([out[r * mx:r * mx + s] for r, s in enumerate(sizes)], dim=0)
 
 
 class ShardedInference(nn.Module):

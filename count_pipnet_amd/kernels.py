@@ -34,35 +34,18 @@ def _launch(kname: str, flops: float, fn) -> None:
         _launch_hook(kname, flops, fn)
 
 
-def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int, agelu: bool = False) -> str:
+def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant and
     launch_gemm in csrc/gemm_f32.hip for dense, unit-stride operands: leading dimensions equal
-    to K / N, 16-B aligned torch allocations -- so ``vec_epi`` holds whenever N % 4 == 0).
-    ``agelu``: pipnet_linear_agelu_f32 (GELU on A-load; the 32-deep tiles only)."""
-    ag = "true" if agelu else "false"
-    if agelu:
-        if k % 32 or (k <= 96 and n > 192 and m > 64):
-            raise RuntimeError(f"GELU on A-load: no 32-deep tile for M={m} N={n} K={k}")
-        if n <= 384 or k <= 192 or m <= 64:
-            return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, 0, 3, 2, 0, {'true' if n % 128 else 'false'}, true>"
-        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, 0, 2, 2, 0, false, true>"
+    to K / N, 16-B aligned torch allocations -- so ``vec_epi`` holds whenever N % 4 == 0)."""
     if k % 16 == 0 and ((k <= 96 and n > 192 and m > 64) or (k % 32 and m > 64)):
-        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false, {ag}>"
+        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if k % 32:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
     if n <= 384 or k <= 192 or m <= 64:
         npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
-        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}, {ag}>"
-    if n % 128 == 0 and n >= 1024 and k % 16 == 0 and 256 <= k <= 512 and m > 64 \
-            and epilogue != _lib.EPI_RESID_ROWSCALE and gemm_bk16x3():
-        return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 3, 2, 0, false, {ag}>"
-    if aload == 0 and n % 128 == 0 and k % 32 == 0 and k >= 256 and epilogue != _lib.EPI_RESID_ROWSCALE \
-            and -(-m // 128) * (n // 128) >= 4 * _num_cus() and max(m * k, n * k, m * n) < 2 ** 31 \
-            and gemm_stream():
-        return f"pipnet_gemm::gemm_f32_tn_stream_kernel<{epilogue}>"
-    if aload == 0 and n % 128 == 0 and gemm_persist():
-        return f"pipnet_gemm::gemm_f32_tn_persist_kernel<{epilogue}>"
-    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false, {ag}>"
+        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
+    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
 
 
 _CUS = {}
@@ -76,45 +59,6 @@ def _num_cus() -> int:
     if d not in _CUS:
         _CUS[d] = torch.cuda.get_device_properties(d).multi_processor_count
     return _CUS[d]
-
-
-def gemm_stream(mode: int = -1) -> bool:
-    """The library's streaming-GEMM switch (include/pipnet_amd.h pipnet_gemm_stream): mode 1 / 0
-    sets it, -1 queries."""
-    r = _lib.load().pipnet_gemm_stream(mode)
-    if r < 0:
-        _lib.check(r, f"pipnet_gemm_stream({mode})")
-    return bool(r)
-
-
-def gemm_plain_store(mode: int = -1) -> int:
-    """The library's store-policy switch of the fp32 GEMM output tiles (include/pipnet_amd.h
-    pipnet_gemm_plain_store): 1 = plain cached stores, 0 = non-temporal (default), -1 queries."""
-    return _lib.load().pipnet_gemm_plain_store(mode)
-
-
-def head_bf16_quads(mode: int = -1) -> int:
-    """The library's layout switch of the bf16 prototype head (include/pipnet_amd.h
-    pipnet_head_bf16_quads): 1 = 4 channels per lane, 0 = 8 per lane, -1 queries."""
-    return _lib.load().pipnet_head_bf16_quads(mode)
-
-
-def gemm_bk16x3(mode: int = -1) -> bool:
-    """The library's 3-workgroups-per-CU tile switch for short-K wide-N GEMMs (include/pipnet_amd.h
-    pipnet_gemm_bk16x3): mode 1 / 0 sets it, -1 queries."""
-    r = _lib.load().pipnet_gemm_bk16x3(mode)
-    if r < 0:
-        _lib.check(r, f"pipnet_gemm_bk16x3({mode})")
-    return bool(r)
-
-
-def gemm_persist(mode: int = -1) -> bool:
-    """The library's persistent-GEMM switch (include/pipnet_amd.h pipnet_gemm_persist): mode 1 / 0
-    sets it, -1 queries."""
-    r = _lib.load().pipnet_gemm_persist(mode)
-    if r < 0:
-        _lib.check(r, f"pipnet_gemm_persist({mode})")
-    return bool(r)
 
 
 SPLITK_WG_PER_CU = int(os.environ.get("PIPNET_SPLITK_WG_PER_CU", "2"))   # env: A/B runs (tools)
@@ -173,7 +117,7 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     splits = splitk_factor(m, n, k)
     if splits > 1:
         ws = torch.empty((splits, m, n), device=a.device, dtype=torch.float32)
-        _launch(f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, 0, 0, 3, 2, 0, false, false>", 2.0 * m * n * k,
+        _launch(f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, 0, 0, 3, 2, 0, false>", 2.0 * m * n * k,
                 lambda: _lib.call("pipnet_linear_splitk_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias),
                                   _ptr(scale), _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue, splits,
                                   ws.data_ptr(), _stream(a)))
@@ -195,33 +139,6 @@ def matmul_f64acc(a: Tensor, b: Tensor) -> Tensor:
     n = b.shape[1]
     out = torch.empty((m, n), device=a.device, dtype=torch.float32)
     _lib.call("pipnet_matmul_f64acc_f32", a.data_ptr(), k, b.data_ptr(), n, out.data_ptr(), n, m, n, k, _stream(a))
-    return out
-
-
-def linear_agelu_ok(m: int, n: int, k: int) -> bool:
-    """Whether pipnet_linear_agelu_f32 serves this shape (a 32-deep tile: mirrors gemm_variant)."""
-    return k % 32 == 0 and n % 4 == 0 and not (k <= 96 and n > 192 and m > 64)
-
-
-def linear_agelu(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = _lib.EPI_NONE,
-                 scale: Optional[Tensor] = None, r: Optional[Tensor] = None, out: Optional[Tensor] = None) -> Tensor:
-    """out[M,N] = epi(gelu_erf(a[M,K]) @ w[N,K]^T), the GELU applied to A as it is loaded
-    (include/pipnet_amd.h pipnet_linear_agelu_f32); epi in {NONE, BIAS, RESID}."""
-    require_device(a, "linear input")
-    _chk(w, "weight")
-    if a.dim() != 2 or w.dim() != 2 or a.stride(1) != 1:
-        raise RuntimeError("linear_agelu: expects 2-D operands with unit column stride")
-    m, k = a.shape
-    n = w.shape[0]
-    if w.shape[1] != k or not linear_agelu_ok(m, n, k):
-        raise RuntimeError(f"linear_agelu: unsupported shape {tuple(a.shape)} x {tuple(w.shape)}")
-    if out is None:
-        out = torch.empty((m, n), device=a.device, dtype=torch.float32)
-    ldr = r.stride(0) if r is not None else 0
-    _launch(gemm_kernel_name(m, n, k, epilogue, 0, agelu=True), 2.0 * m * n * k,
-            lambda: _lib.call("pipnet_linear_agelu_f32", a.data_ptr(), a.stride(0), w.data_ptr(), _ptr(bias),
-                              _ptr(scale), _ptr(r), ldr, out.data_ptr(), out.stride(0), m, n, k, epilogue,
-                              _stream(a)))
     return out
 
 
@@ -346,31 +263,7 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
              4: ("pipnet_bf16::Cfg<2, 2, 2, 2, 32, 4>", 2), 6: ("pipnet_bf16::Cfg<4, 1, 2, 2, 32, 4>", 2)}
 
 
-def conv_bf16_rb(mode: int = -1) -> int:
-    """The library's row-block switch of the 256-wide bf16 ping-pong tiles (include/pipnet_amd.h
-    pipnet_conv_bf16_rb): 7 / 8 force 224- / 256-row tiles, 0 = automatic, 1 / 2 = automatic for
-    the halo / the persistent tile only, -1 queries."""
-    r = _lib.load().pipnet_conv_bf16_rb(mode)
-    if r < 0:
-        _lib.check(-r, f"pipnet_conv_bf16_rb({mode})")
-    return r
-
-
-def bf16_pp_rb(m: int, nt: int, halo: bool = False) -> int:
-    """Row blocks per wave group the library picks for a halo / persistent tile grid of ``nt``
-    256-wide column tiles (mirrors pick_rb in csrc/conv_bf16.hip): 7 (224-row tiles) when that
-    gives fewer tile rounds x tile work per CU, else 8 (256-row tiles)."""
-    mode = conv_bf16_rb(-1) if torch.cuda.is_available() else 8
-    if mode in (7, 8):
-        return mode
-    if (mode == 1 and not halo) or (mode == 2 and halo):
-        return 8
-    cus = _num_cus()
-
-    def cost(rb):
-        tiles = -(-m // (32 * rb)) * nt
-        return -(-tiles // cus) * (1.0 if rb == 8 else 0.875 * 1.03)
-    return 7 if cost(7) < cost(8) else 8
+PP_RB = 8     # row blocks of the 256-wide ping-pong tiles (csrc/conv_bf16.hip PP_RB): 256-row tiles
 
 
 def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True,
@@ -381,11 +274,10 @@ def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int =
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
-        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {bf16_pp_rb(m, n // 256)}>"
+        return f"pipnet_bf16::conv_bf16_ppp_kernel<{epilogue}, {PP_RB}>"
     if t == 8:
         nb = 4 if n >= 256 else (2 if n >= 128 else 1)
-        rb = bf16_pp_rb(m, -(-n // (64 * nb)), halo=True) if nb == 4 else 8
-        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, {nb}, {rb}>"
+        return f"pipnet_bf16::conv3x3_bf16_halo_kernel<{epilogue}, {nb}, {PP_RB}>"
     if t == 5:
         return f"pipnet_bf16::conv_bf16_pp_kernel<{epilogue}, {aload}, 4, 0, 2>"
     if t == 7:
@@ -498,7 +390,7 @@ def conv1x1_bf16_dual(x: Tensor, w_packed: Tensor, bias: Tensor, n1: int, n2: in
     y1 = torch.empty((b, h, w, n1), device=x.device, dtype=torch.bfloat16)
     y2 = torch.empty((b, h, w, n2), device=x.device, dtype=torch.bfloat16)
     m = b * h * w
-    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {bf16_pp_rb(m, (n1 + n2) // 256)}>",
+    _launch(f"pipnet_bf16::conv_bf16_ppp_kernel<12, {PP_RB}>",
             2.0 * m * (n1 + n2) * cin,
             lambda: _lib.call("pipnet_conv1x1_bf16_dual", x.data_ptr(), m, cin, w_packed.data_ptr(), bias.data_ptr(),
                               n1, y1.data_ptr(), n2, y2.data_ptr(), _stream(x)))
@@ -710,6 +602,43 @@ def softmax_pool(feat_nhwc: Tensor, pool_mode: int, out=None) -> Tuple[Tensor, T
     _lib.call("pipnet_softmax_pool_f32", feat_nhwc.data_ptr(), b, h * w, p, pool_mode, proto.data_ptr(),
               pooled.data_ptr(), _stream(feat_nhwc))
     return proto, pooled
+
+
+def softmax_pool_linear(feat_nhwc: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float],
+                        out=None) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """The PIP-Net head in one launch (pipnet.py:33-37): fp32 or bf16 logits [B,h,w,P] ->
+    (proto [B,h,w,P], pooled [B,P], x' [B,P], logits [B,K]) with x' = where(pooled < thresh, 0,
+    pooled) (or pooled when ``thresh`` is None) and logits = x' relu(w)^T + bias, w read at call
+    time.  ``out`` = (proto, pooled, x', logits) to write into (batch slices of a larger output).
+    Bitwise equal to softmax_pool(..., 0) + nonneg_linear."""
+    bf = feat_nhwc.dtype == torch.bfloat16
+    if bf:
+        _chk_bf(feat_nhwc, "prototype logits")
+    else:
+        _chk(feat_nhwc, "prototype logits")
+    _chk(w, "classifier weight")
+    b, h, wd, p = feat_nhwc.shape
+    k = w.shape[0]
+    if w.dim() != 2 or w.shape[1] != p:
+        raise RuntimeError(f"softmax_pool_linear: weight {tuple(w.shape)} vs {p} prototypes")
+    dev = feat_nhwc.device
+    if out is None:
+        proto, pooled = _head_out(None, b, h, wd, p, dev)
+        x_out = torch.empty((b, p), device=dev, dtype=torch.float32)
+        logits = torch.empty((b, k), device=dev, dtype=torch.float32)
+    else:
+        proto, pooled = _head_out((out[0], out[1]), b, h, wd, p, dev)
+        x_out, logits = out[2], out[3]
+        if tuple(x_out.shape) != (b, p) or tuple(logits.shape) != (b, k):
+            raise RuntimeError("softmax_pool_linear: out shapes do not match")
+        _chk(x_out, "classifier input out")
+        _chk(logits, "logits out")
+    tickets = torch.empty((b,), device=dev, dtype=torch.int32)       # zeroed by the launch
+    _lib.call("pipnet_softmax_pool_linear_bf16" if bf else "pipnet_softmax_pool_linear_f32", feat_nhwc.data_ptr(), b,
+              h * wd, p, proto.data_ptr(), pooled.data_ptr(), w.data_ptr(), _ptr(bias), k,
+              0 if thresh is None else 1, 0.0 if thresh is None else float(thresh), x_out.data_ptr(),
+              logits.data_ptr(), tickets.data_ptr(), _stream(feat_nhwc))
+    return proto, pooled, x_out, logits
 
 
 def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float],

@@ -22,7 +22,7 @@ from torch import Tensor
 
 from . import _lib
 from . import kernels as K
-from .backend import use_hip
+from .backend import cross_stream_forward, use_hip
 from .convnext_features import as_nhwc, convnext_tiny_13_features, convnext_tiny_26_features, nhwc_as_nchw
 from .resnet_features import (resnet18_features, resnet34_features, resnet50_features, resnet50_features_inat,
                               resnet101_features, resnet152_features)
@@ -61,7 +61,8 @@ class PIPNet(nn.Module):
         if not (isinstance(self._pool, nn.Sequential) and isinstance(self._pool[0], nn.AdaptiveMaxPool2d)):
             raise RuntimeError("PIPNet HIP path expects _pool = Sequential(AdaptiveMaxPool2d(1), Flatten())")
         if stream_split(self, xs) > 1:
-            return self._forward_hip_split(xs, inference, stream_split(self, xs))
+            with cross_stream_forward():
+                return self._forward_hip_split(xs, inference, stream_split(self, xs))
         logits = self._hip_logits(xs)
         proto, pooled, clamped, out = self._hip_head(logits, inference)
         return nhwc_as_nchw(proto), (clamped if inference else pooled), out
@@ -71,17 +72,13 @@ class PIPNet(nn.Module):
         return add_on_logits_hip(self._add_on, feats)      # [B,h,w,P]
 
     def _hip_head(self, logits: Tensor, inference: bool, out=None):
-        """softmax + max-pool + threshold + NonNegLinear; ``out`` = (proto, pooled, clamped,
-        logits) tensors to write into (batch slices of the split forward)."""
-        po = None if out is None else (out[0], out[1])
-        if logits.dtype == torch.bfloat16:
-            proto, pooled = K.softmax_pool_bf16(logits, pool_mode=0, out=po)
-        else:
-            proto, pooled = K.softmax_pool(logits, pool_mode=0, out=po)
+        """softmax + max-pool + threshold + NonNegLinear as ONE kernel launch (the classifier runs
+        in the last workgroup of each image, include/pipnet_amd.h pipnet_softmax_pool_linear_f32);
+        ``out`` = (proto, pooled, clamped, logits) tensors to write into (batch slices of the
+        split forward)."""
         cls = self._classification
-        lo = None if out is None else (out[2], out[3])
-        clamped, res = K.nonneg_linear(pooled, cls.weight, cls.bias, PRESENCE_THRESHOLD if inference else None,
-                                       out=lo)
+        proto, pooled, clamped, res = K.softmax_pool_linear(
+            logits, cls.weight, cls.bias, PRESENCE_THRESHOLD if inference else None, out=out)
         return proto, pooled, clamped, res
 
     def _forward_hip_split(self, xs: Tensor, inference: bool, n: int):

@@ -48,8 +48,12 @@ extern "C" {
 #define PIPNET_EPI_DUAL_BIAS_RELU 12 /* columns < N1: C = A W^T + b; columns >= N1: C2 = relu(A W^T + b) (bf16 1x1 convs, pipnet_conv1x1_bf16_dual) */
 
 /* ABI version: bumped whenever an exported signature changes.  2: pipnet_wgrad_conv_f32 gained
- * its `pad` argument (round 2); a caller built against version 1 must not bind this library. */
-#define PIPNET_AMD_ABI_VERSION 2
+ * its `pad` argument (round 2).  3: the process-wide A/B switches (pipnet_gemm_persist /
+ * _stream / _bk16x3 / _plain_store, pipnet_conv_bf16_rb, pipnet_head_bf16_quads) and
+ * pipnet_linear_agelu_f32 are gone -- kernel selection is a fixed per-shape rule with no
+ * mutable library state -- and the fused head pipnet_softmax_pool_linear_f32 / _bf16 is new
+ * (round 5).  A caller built against an older version must not bind this library. */
+#define PIPNET_AMD_ABI_VERSION 3
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
 /* sha256 (hex) of the sources this library was compiled from (build provenance). */
@@ -65,50 +69,6 @@ const char* pipnet_amd_source_digest(void);
 int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
                       const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                       int M, int N, int K, int epilogue, void* stream);
-
-/* Dense fp32 linear with GELU applied to the A operand as it is loaded:
- *   C[M,N] (ldc) = epi( gelu_erf(A[M,K]) (lda) * W[N,K]^T ),  epi in {NONE, BIAS, RESID}
- * The CNBlock MLP (torchvision block.3 Linear, block.4 GELU, block.5 Linear + layer_scale +
- * residual) runs as pipnet_linear_f32(EPI_BIAS) + this call (EPI_RESID): the GELU moves from
- * Linear1's epilogue into Linear2's main loop, bitwise the same result.  K % 32 == 0, N % 4 == 0,
- * lda / ldc / ldr % 4 == 0, 16-B aligned operands, and a shape served by the 32-deep tiles
- * (K > 96): PIPNET_ERR_ARG otherwise (use the EPI_BIAS_GELU epilogue then). */
-int pipnet_linear_agelu_f32(const float* A, int64_t lda, const float* W, const float* bias,
-                            const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
-                            int M, int N, int K, int epilogue, void* stream);
-
-/* Persistent 128x128 fp32 GEMM tile for the 128-row / 2-stage shapes with N % 128 == 0
- * (stage-3/4 CNBlock Linears): mode 1 on, 0 off, -1 query only.  Returns the mode in force
- * (initially PIPNET_GEMM_PERSIST from the environment, else the build default) or a
- * negative status.  Not thread-safe against concurrent launches (process-wide A/B switch). */
-int pipnet_gemm_persist(int mode);
-
-/* 3-workgroups-per-CU fp32 GEMM tile (128 rows, 16-deep K-tiles, 2 LDS stages) for the short-K
- * wide-N GEMMs (N % 128 == 0, N >= 1024, 256 <= K <= 512: the stage-3 CNBlock Linear1 + GELU):
- * mode 1 on, 0 off, -1 query.  Returns the mode in force (initially PIPNET_GEMM_BK16X3 from the
- * environment, else the build default) or a negative status.  Its 32x32x2 MFMAs pair k with
- * k + 8 instead of k + 16 (a different fp32 summation order, exact-fp32 products either way);
- * the choice depends on the layer's N and K only, so results stay batch-invariant.
- * Process-wide switch, not thread-safe against concurrent launches. */
-/* Store policy of the fp32 GEMM output tiles (pipnet_linear_f32 / conv paths): 1 = plain
- * (cached) stores, 0 = non-temporal (default); -1 queries.  Same bits either way.  Process-wide A/B
- * switch, not thread-safe against concurrent launches. */
-/* Layout of the bf16 prototype head (pipnet_softmax_pool_bf16): 1 = 4 channels per lane (8-B
- * loads, 16-B proto stores covering whole lines; default), 0 = 8 channels per lane; -1 queries.
- * The softmax denominators' partial sums group differently (last-bit differences).  Process-wide
- * A/B switch, not thread-safe against concurrent launches. */
-int pipnet_head_bf16_quads(int mode);
-int pipnet_gemm_plain_store(int mode);
-int pipnet_gemm_bk16x3(int mode);
-
-/* Streaming persistent 128x128 fp32 GEMM tile (stage-3/4 CNBlock Linears: N % 128 == 0,
- * K % 32 == 0, K >= 256, >= 4 tiles per CU): two workgroups per CU walk their tiles as one
- * stream of K-tiles and each tile's epilogue runs sliced under the next tile's main loop.
- * Bitwise equal to the regular tile.  mode 1 on, 0 off, -1 query only; returns the mode in
- * force (initially PIPNET_GEMM_STREAM from the environment, else off: 3-5 % slower than the
- * regular tile on the stage-3/4 shapes, profiles/r03/gemm_stream_ab.txt) or a negative status.
- * Takes precedence over pipnet_gemm_persist.  Process-wide A/B switch. */
-int pipnet_gemm_stream(int mode);
 
 /* pipnet_linear_f32 with PIPNET_EPI_RESID_ROWSCALE: C = R + row_scale[m / rows_per_scale] *
  * (scale * (A W^T + bias)).  The CNBlock's Linear2 * layer_scale + residual under
@@ -260,6 +220,20 @@ int pipnet_stem_pool_bf16(const void* s2d, int B, int SH, int SW, const void* w,
 /* pipnet_softmax_pool_f32 reading bf16 logits (fp32 softmax, fp32 proto / pooled out). */
 int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mode, float* proto,
                              float* pooled, void* stream);
+
+/* The whole PIP-Net head in ONE kernel launch (pipnet.py:33-37; replaces pipnet_softmax_pool_f32
+ * (pool_mode 0) + pipnet_nonneg_linear_f32): per-pixel softmax over P channels, proto written
+ * once, spatial max into pooled [B,P], then -- in the last workgroup to finish image b (an
+ * arrival ticket) -- x' = where(pooled < thresh, 0, pooled) when apply_thresh, else pooled,
+ * written to x_out [B,P] (may be NULL), and out [B,K] = x' relu(W)^T + bias, W [K,P] read at
+ * call time.  tickets: int32 [B] workspace (zeroed by this call together with pooled).  Bitwise
+ * equal to the two-kernel path.  W 16-B aligned when P % 4 == 0.  _bf16: bf16 logits. */
+int pipnet_softmax_pool_linear_f32(const float* feat, int B, int HW, int P, float* proto, float* pooled,
+                                   const float* W, const float* bias, int K, int apply_thresh, float thresh,
+                                   float* x_out, float* out, int32_t* tickets, void* stream);
+int pipnet_softmax_pool_linear_bf16(const void* feat, int B, int HW, int P, float* proto, float* pooled,
+                                    const float* W, const float* bias, int K, int apply_thresh, float thresh,
+                                    float* x_out, float* out, int32_t* tickets, void* stream);
 
 /* ---- eval_pipnet metric loop (pipnet/test.py:67-131,266-319) -------
  * One evaluation batch, entirely on the device (no host sync):
@@ -496,15 +470,6 @@ int pipnet_onehot_ste_bwd_f32(const float* x, int64_t rows, int M, const float* 
 int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, int HW, int P, const float* d_counts_in,
                               float w_align, float w_tanh, float tanh_coeff, float inv_tau, float* dcnt_ws,
                               float* d_logits, void* stream);
-
-/* Row blocks of the 256-wide bf16 ping-pong tiles (the LDS-halo 3x3 tile and the persistent 1x1
- * tile): mode 7 forces 224-row tiles, 8 forces 256-row tiles (the default: C3's two concurrent
- * streams fill short last rounds already), 0 = the automatic choice (the form with fewer tile
- * rounds per CU, conv_bf16.hip pick_rb: faster for one-stream callers), 1 / 2 = automatic for the
- * halo / the persistent tile only, -1 queries; initially PIPNET_PP_RB from the environment.  Returns the mode in force or a negative status.  Both forms compute
- * every output element with the same MFMA chain over the same K order: bitwise equal outputs.
- * Process-wide A/B switch, not thread-safe against concurrent launches. */
-int pipnet_conv_bf16_rb(int mode);
 
 /* fp64-accumulated product for inference-time weight folds (csrc/fold_f64.hip):
  *   C[M,N] (ldc) = RNE_f32( sum_k double(A[m,k]) * double(B[k,n]) ), A [M,K] (lda) and B [K,N]

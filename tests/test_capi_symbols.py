@@ -25,7 +25,7 @@ def test_library_loads_and_exports_all_symbols():
     lib = _lib.load()
     for s in declared_symbols():
         assert hasattr(lib, s), s
-    assert lib.pipnet_amd_abi_version() == 2
+    assert lib.pipnet_amd_abi_version() == 3
     assert lib.pipnet_amd_status_string(1).decode().startswith("invalid argument")
 
 

@@ -351,54 +351,16 @@ def test_cnblock_mlp_batch_invariant(gpu, c, m):
 
 
 @pytest.mark.parametrize("m,n,k,epi", [
-    (46656 // 4, 1536, 384, "gelu"),     # stage-3 fc1 shape (quarter batch): several tiles per workgroup
-    (10000, 3072, 768, "gelu"),          # stage-4 fc1 shape, ragged M
-    (46656 // 4, 512, 1536, "resid"),    # residual epilogue on the persistent tile
-    (300, 256, 512, "none"),             # fewer tiles than workgroups
-])
-def test_gemm_persistent_bitwise(gpu, m, n, k, epi):
-    """The persistent fp32 GEMM tile (pipnet_gemm_persist) keeps the K order and the epilogue
-    arithmetic of the 128x128 tile: outputs bitwise equal, including across tile switches
-    (next tile's K-tile 0 in flight during the epilogue) and the clamped rows past M."""
-    g = torch.Generator().manual_seed(m + n + k)
-    a = torch.randn(m, k, generator=g).to(gpu)
-    w = (torch.randn(n, k, generator=g) * 0.05).to(gpu)
-    b = torch.randn(n, generator=g).to(gpu)
-    s = torch.randn(n, generator=g).to(gpu)
-    r = torch.randn(m, n, generator=g).to(gpu)
-    e = {"gelu": _lib.EPI_BIAS_GELU, "resid": _lib.EPI_RESID, "none": _lib.EPI_NONE}[epi]
-    prev = K.gemm_persist()
-    try:
-        outs = []
-        for mode in (0, 1):
-            K.gemm_persist(mode)
-            outs.append(K.linear(a, w, b, e, scale=s, r=r if epi == "resid" else None))
-        torch.cuda.synchronize()
-    finally:
-        K.gemm_persist(int(prev))
-    assert torch.equal(outs[0], outs[1])
-    ref = a.double() @ w.double().t()
-    if epi == "gelu":
-        ref = torch.nn.functional.gelu(ref + b.double())
-    elif epi == "resid":
-        ref = r.double() + s.double() * (ref + b.double())
-    assert (outs[1].double() - ref).abs().max().item() < 1e-3
-
-
-@pytest.mark.parametrize("m,n,k,epi", [
-    (46656 // 2, 1536, 384, "gelu"),     # stage-3 fc1 shape (half batch): many tiles per workgroup
-    (46656, 1536, 384, "gelu"),          # stage-3 fc1, full C2 batch
+    (46656 // 2, 1536, 384, "gelu"),     # stage-3 fc1 shape (half batch)
     (20001, 3072, 768, "gelu"),          # stage-4 fc1 shape, ragged M (last tile 33 rows)
-    (43264, 768, 3072, "resid"),         # stage-4 fc2: residual epilogue, K = 3072
-    (30000, 1024, 256, "none"),          # K = 256: exactly 8 K-tiles per tile (one slice each)
+    (43264 // 4, 768, 3072, "resid"),    # stage-4 fc2: residual epilogue in place, K = 3072
     (30001, 1024, 512, "bias"),          # bias epilogue, ragged M
+    (300, 256, 512, "none"),             # fewer tiles than CUs
 ])
-def test_gemm_stream_bitwise(gpu, m, n, k, epi):
-    """The streaming tile (pipnet_gemm_stream: K-tiles of consecutive tiles as one DMA stream,
-    each tile's epilogue sliced under the next tile's main loop, stores from the MFMA layout)
-    against the regular 128x128 tile: bitwise equal, rows past M never written, and within
-    1e-3 of an fp64 reference.  The residual case runs in place (R aliases C, as the CNBlock
-    residual stream does)."""
+def test_gemm_product_tile_vs_fp64(gpu, m, n, k, epi):
+    """The product 128x128 fp32 tile on the stage-3/4 CNBlock shapes: within 1e-3 of an fp64
+    reference, rows past M never written, the residual case in place (R aliases C, as the
+    CNBlock residual stream does)."""
     g = torch.Generator().manual_seed(m + n + k)
     a = torch.randn(m, k, generator=g).to(gpu)
     w = (torch.randn(n, k, generator=g) * 0.05).to(gpu)
@@ -406,28 +368,16 @@ def test_gemm_stream_bitwise(gpu, m, n, k, epi):
     s = torch.randn(n, generator=g).to(gpu)
     r = torch.randn(m, n, generator=g).to(gpu)
     e = {"gelu": _lib.EPI_BIAS_GELU, "resid": _lib.EPI_RESID, "none": _lib.EPI_NONE, "bias": _lib.EPI_BIAS}[epi]
-    prev = K.gemm_stream()
-    try:
-        outs = []
-        for mode in (0, 1):
-            K.gemm_stream(mode)
-            assert ("stream" in K.gemm_kernel_name(m, n, k, e, 0)) == bool(mode)
-            if epi == "resid":
-                buf = torch.empty(m + 7, n, device=gpu)
-                buf[m:] = 12345.0                                   # rows past M: must stay untouched
-                buf[:m] = r
-                K.linear(a, w, b, e, scale=s, r=buf[:m], out=buf[:m])
-                outs.append(buf)
-            else:
-                buf = torch.full((m + 7, n), 12345.0, device=gpu)
-                K.linear(a, w, b, e, scale=s, out=buf[:m])
-                outs.append(buf)
-        torch.cuda.synchronize()
-    finally:
-        K.gemm_stream(int(prev))
-    diff = (outs[0] - outs[1]).abs()
-    assert torch.equal(outs[0], outs[1]), (int((diff > 0).sum()), float(diff.max()), (diff > 0).nonzero()[:4].tolist())
-    assert torch.all(outs[1][m:] == 12345.0)
+    if epi == "resid":
+        buf = torch.empty(m + 7, n, device=gpu)
+        buf[m:] = 12345.0                                   # rows past M: must stay untouched
+        buf[:m] = r
+        K.linear(a, w, b, e, scale=s, r=buf[:m], out=buf[:m])
+    else:
+        buf = torch.full((m + 7, n), 12345.0, device=gpu)
+        K.linear(a, w, b, e, scale=s, out=buf[:m])
+    torch.cuda.synchronize()
+    assert torch.all(buf[m:] == 12345.0)
     ref = a.double() @ w.double().t()
     if epi == "gelu":
         ref = torch.nn.functional.gelu(ref + b.double())
@@ -435,56 +385,63 @@ def test_gemm_stream_bitwise(gpu, m, n, k, epi):
         ref = r.double() + s.double() * (ref + b.double())
     elif epi == "bias":
         ref = ref + b.double()
-    assert (outs[1][:m].double() - ref).abs().max().item() < 1e-3
+    assert (buf[:m].double() - ref).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("m,c,hid", [(2000, 384, 1536), (1000, 768, 3072), (1234, 96, 384), (777, 192, 768)])
-def test_linear_agelu_bitwise_equals_gelu_epilogue(gpu, m, c, hid):
-    """pipnet_linear_agelu_f32 (GELU applied to Linear2's A fragments in registers) gives bit for
-    bit the EPI_BIAS_GELU Linear1 + plain Linear2 path of the CNBlock MLP (same gelu_pk16 of the
-    same fp32 values, same MFMA chain): 128-row tiles (stage 3/4 widths), 64-row tiles (N <= 384)
-    and the padded-column (N % 128 != 0) instantiation, the residual epilogue in place."""
-    from count_pipnet_amd import kernels as K, _lib
-    g = torch.Generator().manual_seed(m + c)
-    t = torch.randn(m, c, generator=g).to(gpu)
-    w1 = (torch.randn(hid, c, generator=g) / c ** 0.5).to(gpu)
-    b1 = torch.randn(hid, generator=g).to(gpu)
-    w2 = (torch.randn(c, hid, generator=g) / hid ** 0.5).to(gpu)
-    b2 = torch.randn(c, generator=g).to(gpu)
-    ls = torch.rand(c, generator=g).to(gpu)
-    x = torch.randn(m, c, generator=g).to(gpu)
-    u_gelu = K.linear(t, w1, b1, _lib.EPI_BIAS_GELU)
-    y_ref = x.clone()
-    K.linear(u_gelu, w2, b2, _lib.EPI_RESID, scale=ls, r=y_ref, out=y_ref)
-    u_pre = K.linear(t, w1, b1, _lib.EPI_BIAS)
-    y = x.clone()
-    K.linear_agelu(u_pre, w2, b2, _lib.EPI_RESID, scale=ls, r=y, out=y)
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("b,hw,p,k,thresh", [
+    (64, 26 * 26, 768, 200, 0.1),     # C2 head (inference: 0.1 presence threshold)
+    (5, 26 * 26, 768, 200, None),     # raw mode: x' = pooled
+    (3, 28 * 28, 2048, 200, 0.1),     # C3 head (P = 2048)
+    (4, 7 * 7, 96, 9, 0.1),           # K < 16, one pixel block per image
+    (2, 33, 20, 3, 0.1),              # P % 8 != 0 (bf16 takes the lane-strided kernel), ragged pixel block
+    (2, 100, 130, 37, None),          # P % 4 != 0: the scalar GEMV slices
+])
+def test_fused_head_bitwise_two_kernel_path(gpu, dtype, b, hw, p, k, thresh):
+    """pipnet_softmax_pool_linear_{f32,bf16} (the NonNegLinear in each image's last workgroup,
+    one launch) against pipnet_softmax_pool + pipnet_nonneg_linear (two launches): proto,
+    pooled, x' and logits bitwise equal; logits within 1e-5 of an fp64 reference."""
+    g = torch.Generator().manual_seed(b * 7 + p + k)
+    feat = (torch.randn(b, hw, p, generator=g) * 3).to(gpu)
+    if dtype == "bf16":
+        feat = feat.to(torch.bfloat16)
+    w = torch.randn(k, p, generator=g).to(gpu)          # negative entries: relu(W) matters
+    bias = torch.randn(k, generator=g).to(gpu)
+    h = 1
+    f4 = feat.view(b, h, hw, p)
+    proto, pooled, xo, out = K.softmax_pool_linear(f4, w, bias, thresh)
+    if dtype == "bf16":
+        proto2, pooled2 = K.softmax_pool_bf16(f4, 0)
+    else:
+        proto2, pooled2 = K.softmax_pool(f4, 0)
+    xo2, out2 = K.nonneg_linear(pooled2, w, bias, thresh)
     torch.cuda.synchronize()
-    assert torch.equal(y, y_ref)
-    # and against fp64 torch (exact GELU) at fp32 tolerance
-    ref = x.double() + ls.double() * (torch.nn.functional.gelu(t.double() @ w1.double().t() + b1.double())
-                                      @ w2.double().t() + b2.double())
-    assert (y.double() - ref).abs().max().item() < 1e-4 * max(1.0, ref.abs().max().item())
+    assert torch.equal(proto, proto2)
+    assert torch.equal(pooled, pooled2)
+    assert torch.equal(xo, xo2)
+    assert torch.equal(out, out2)
+    xr = pooled.double()
+    if thresh is not None:
+        xr = torch.where(xr < thresh, 0.0, xr)
+    ref = xr @ w.double().clamp_min(0).t() + bias.double()
+    assert (out.double() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+    # a second call on reused (non-zero) buffers: tickets and pooled are re-zeroed by the launch
+    proto3, pooled3, xo3, out3 = K.softmax_pool_linear(f4, w, bias, thresh, out=(proto, pooled, xo, out.clone()))
+    torch.cuda.synchronize()
+    assert torch.equal(out3, out2) and torch.equal(pooled3, pooled2)
 
 
-def test_defer_gelu_network_bitwise(gpu):
-    """C2's CNBlocks with the GELU on Linear2's A-load (the default) and in Linear1's epilogue give
-    bitwise the same network outputs."""
-    from count_pipnet_amd import convnext_features as CF
-    from count_pipnet_amd.synthetic import synth_images
-    from golden_util import load_golden
-    from model_util import build_model
-    meta, _ = load_golden("c2_pipnet_convnext26")
-    net = build_model(meta).to(gpu).eval()
-    xs = synth_images(3, 224, seed=9).to(gpu)
-    outs = {}
-    prev = CF.DEFER_GELU
-    try:
-        for flag in (False, True):
-            CF.DEFER_GELU = flag
-            with torch.no_grad():
-                outs[flag] = [o.clone() for o in net(xs, inference=True)]
-    finally:
-        CF.DEFER_GELU = prev
-    for a, b in zip(outs[False], outs[True]):
-        assert torch.equal(a, b)
+def test_fused_head_reads_weight_at_call_time(gpu):
+    """The fused head reads W when it runs: an in-place clamp between two calls (test.py:71-73)
+    changes the logits exactly as the two-kernel path does."""
+    g = torch.Generator().manual_seed(3)
+    feat = torch.randn(4, 1, 49, 64, generator=g).to(gpu)
+    w = torch.randn(10, 64, generator=g).to(gpu)
+    _, _, _, out_a = K.softmax_pool_linear(feat, w, None, 0.1)
+    out_a = out_a.clone()
+    w.sub_(0.5).clamp_(min=0)
+    _, pooled, _, out_b = K.softmax_pool_linear(feat, w, None, 0.1)
+    _, ref = K.nonneg_linear(pooled, w, None, 0.1)
+    torch.cuda.synchronize()
+    assert torch.equal(out_b, ref)
+    assert not torch.equal(out_a, out_b)

@@ -5,8 +5,7 @@
 e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3  (arms False, True)
 Stream splits as arms: streams:1:2:3.
 A library switch function instead of a module flag: fn:<module>.<func>:<arg>:<arg>[:<arg>...],
-one arm per argument, e.g. fn:count_pipnet_amd.kernels.conv_bf16_rb:8:0:1 (256-row tiles, the
-automatic choice, automatic for the halo tile only).  Prints one JSON line per arm and whether
+one arm per argument, e.g. fn:module.setter:0:1 (a setter function called with each value).  Prints one JSON line per arm and whether
 every arm's outputs are bitwise equal to the first arm's."""
 import argparse
 import importlib

@@ -41,7 +41,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tiles", default="9,5")
-    ap.add_argument("--rb", default="8", help="row-block forms of tile 9 to time (7 = 224-row tiles)")
     ap.add_argument("--only", default=None)
     a = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -56,13 +55,11 @@ def main():
         wb = w.to(torch.bfloat16)
         b = torch.randn(n, device=dev, generator=g)
         x2 = x.view(m, k)
-        def conv(t, rb):
-            K.conv_bf16_rb(rb)
+        def conv(t):
             return K.conv2d_nhwc_bf16(x, wp, 1, 1, b, 1, 0, _lib.EPI_BIAS_RELU, None, tile=t)
         fns = {}
         for t in tiles:
-            for rb in ([int(v) for v in a.rb.split(",")] if t == 9 else [8]):
-                fns[f"t{t}" + (f"r{rb}" if t == 9 else "")] = (lambda t=t, rb=rb: conv(t, rb))
+            fns[f"t{t}"] = (lambda t=t: conv(t))
         fns["lib"] = lambda: torch.nn.functional.linear(x2, wb)
         for f in fns.values():
             f(), f()
@@ -74,7 +71,6 @@ def main():
         flops = 2.0 * m * n * k
         tiles256 = -(-m // 256) * -(-n // 256)
         line = f"{name:8s} M={m:6d} N={n:5d} K={k:5d} tiles256={tiles256:5d} waves={tiles256 / 256:5.2f}"
-        K.conv_bf16_rb(8)
         for key, v in res.items():
             ms = sorted(v)[len(v) // 2]
             line += f"  {key}: {flops / ms / 1e9:7.1f} TF ({ms * 1e3:7.1f} us)"

@@ -41,9 +41,6 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None, help="comma-separated layer names")
     ap.add_argument("--tiles", default="-1,0,1,2,3,4,5")
-    ap.add_argument("--rb-ab", action="store_true",
-                    help="time the automatic tile twice: 256-row ping-pong tiles forced (r8) and the automatic "
-                         "224/256-row choice (rA) -- kernels.conv_bf16_rb")
     ap.add_argument("--rotate", type=int, default=1,
                     help="cycle through this many input / identity / output buffer sets, so a layer's "
                          "working set exceeds the 256 MB Infinity Cache as it does in the network")
@@ -54,8 +51,6 @@ def main():
     build.build()
     dev = torch.device("cuda:0")
     tiles = [int(t) for t in a.tiles.split(',')]
-    if a.rb_ab:
-        tiles = ["r8", "rA"]
     total = {t: 0.0 for t in tiles}
     for name, h, cin, cout, k, s, pad, epi, cnt in LAYERS:
         if a.only and name not in a.only.split(","):
@@ -74,9 +69,7 @@ def main():
         auto = K.bf16_conv_tile(a.batch * oh * oh, cout, kv=k * k * cin, halo_ok=halo, ppp_ok=ppp, halo64_ok=h64)
         line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={auto}"
         for t in tiles:
-            if isinstance(t, str):          # --rb-ab: automatic tile, row-block mode r8 / rA
-                K.conv_bf16_rb(8 if t == "r8" else 0)
-            ti = -1 if isinstance(t, str) else t
+            ti = t
             try:
                 for _ in range(2):
                     K.conv2d_nhwc_bf16(x, w, k, k, b, s, pad, epi, r, tile=ti)

@@ -1,6 +1,6 @@
 // Tuning lab for the fp32 MFMA GEMM (not part of the product ABI): variants of
 // count_pipnet_amd/csrc/gemm_f32_impl.hpp behind one entry point, for A/B timing in one process.
-#include "../count_pipnet_amd/csrc/gemm_f32_impl.hpp"
+#include "gemm_variants_lab.hpp"
 
 using namespace pipnet_gemm;
 
@@ -84,6 +84,21 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 41: launch<32, 1, 2, 2, 0, 1>(p, epi, s); break;
     case 70: launch<32, 2, 2, 2, 8, 1>(p, epi, s); break;
     case 37: launch<16, 2, 3, 3, 8>(p, epi, s); break;    // v7 with stamps
+    // persistent (50) and streaming persistent (51) 128x128 tiles, 2 workgroups per CU (N % 128 == 0)
+    case 50:
+    case 51: {
+      int cus = 256, dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      p.mt = (p.M + 127) / 128;
+      const int nt = p.mt * p.nt;
+      const dim3 grid(nt < 2 * cus ? nt : 2 * cus), block(NTHREADS);
+      if (variant == 50 && epi == PIPNET_EPI_BIAS_GELU) hipLaunchKernelGGL((gemm_f32_tn_persist_kernel<PIPNET_EPI_BIAS_GELU>), grid, block, 0, s, p);
+      else if (variant == 50) hipLaunchKernelGGL((gemm_f32_tn_persist_kernel<PIPNET_EPI_RESID>), grid, block, 0, s, p);
+      else if (epi == PIPNET_EPI_BIAS_GELU) hipLaunchKernelGGL((gemm_f32_tn_stream_kernel<PIPNET_EPI_BIAS_GELU>), grid, block, 0, s, p);
+      else hipLaunchKernelGGL((gemm_f32_tn_stream_kernel<PIPNET_EPI_RESID>), grid, block, 0, s, p);
+      break;
+    }
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 3;
