@@ -29,6 +29,7 @@ SIGNATURES = {
     "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],
     "pipnet_linear_splitk_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, I32, P, P],
     "pipnet_matmul_f64acc_f32": [P, I64, P, I64, P, I64, I32, I32, I32, P],
+    "pipnet_matmul2_f64acc_f32": [P, P, I64, P, I64, P, P, I64, I32, I32, I32, P],
     "pipnet_conv2x2_f32": [P, I32, I32, I32, I32, P, P, I32, I32, P, P],
     "pipnet_convnext_stem_f32": [P, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_conv2d_nhwc_f32": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, P],

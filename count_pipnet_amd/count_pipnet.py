@@ -216,7 +216,8 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
     once to fp32) turn the inference intermediate into two M = batch GEMMs with K = P that
     stream 2 D P instead of D P + 2 D^2 weight floats (C5: 101 MB instead of 352 MB, 3.5x fewer
     FLOPs) -- the same kind of inference-time fold as the BatchNorm fold of the ResNet path.
-    The products run on the in-tree fp64 MFMA kernel (``K.matmul_f64acc``), never a vendor GEMM.
+    Both products run as one launch of the in-tree fp64 MFMA kernel (``K.matmul2_f64acc``), never
+    a vendor GEMM.
     Rebuilt whenever any of the three weights changes (storage pointer / in-place version); a
     write through ``param.data`` bypasses the version counter -- call
     ``count_pipnet_amd.invalidate_weight_caches(net)`` after one (backend.py)."""
@@ -228,8 +229,7 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
     if ent is None or ent[0] != stamp:
         with torch.no_grad():
             e = layer.embed.weight.detach().contiguous()
-            wf = K.matmul_f64acc(layer.W.weight.detach().contiguous(), e)
-            vf = K.matmul_f64acc(layer.V.weight.detach().contiguous(), e)
+            wf, vf = K.matmul2_f64acc(layer.W.weight.detach().contiguous(), layer.V.weight.detach().contiguous(), e)
         ent = (stamp, (wf, vf))
         cache[key] = ent
         packed_ready()

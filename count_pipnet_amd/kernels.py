@@ -142,6 +142,21 @@ def matmul_f64acc(a: Tensor, b: Tensor) -> Tensor:
     return out
 
 
+def matmul2_f64acc(a0: Tensor, a1: Tensor, b: Tensor) -> Tuple[Tensor, Tensor]:
+    """(a0 @ b, a1 @ b) as ``matmul_f64acc`` in ONE launch (pipnet_matmul2_f64acc_f32): the
+    bilinear fold's W.E and V.E share the embedding operand."""
+    for t, what in ((a0, "fold operand A0"), (a1, "fold operand A1"), (b, "fold operand B")):
+        _chk(t, what)
+    if a0.dim() != 2 or a0.shape != a1.shape or b.dim() != 2 or a0.shape[1] != b.shape[0]:
+        raise RuntimeError(f"matmul2_f64acc: shapes {tuple(a0.shape)}, {tuple(a1.shape)} x {tuple(b.shape)}")
+    m, k = a0.shape
+    n = b.shape[1]
+    out = torch.empty((2, m, n), device=a0.device, dtype=torch.float32)
+    _lib.call("pipnet_matmul2_f64acc_f32", a0.data_ptr(), a1.data_ptr(), k, b.data_ptr(), n, out[0].data_ptr(),
+              out[1].data_ptr(), n, m, n, k, _stream(a0))
+    return out[0], out[1]
+
+
 def linear_rowscale(a: Tensor, w: Tensor, bias: Optional[Tensor], scale: Tensor, r: Tensor, row_scale: Tensor,
                     rows_per_scale: int) -> Tensor:
     """In place on ``r`` ([M,N]): r = r + row_scale[m // rows_per_scale] * (scale * (a w^T + bias))
@@ -326,6 +341,7 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
     pp_ok = (aload == 0 or cin % 32 == 0) and kp % 32 == 0
     halo_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin % 64 == 0 and w <= 31 and cout >= 256
+               and b * h * w * cin < 2 ** 31          # conv_bf16.hip halo_ok: 32-bit halo source offsets
                and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
     ppp_ok = (aload == 0 and pp_ok and cout % 256 == 0
               and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))

@@ -479,6 +479,11 @@ int pipnet_count_head_bwd_f32(const float* proto, const float* counts, int Bh, i
  * run once per weight version, off the steady-state forward. */
 int pipnet_matmul_f64acc_f32(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                              int M, int N, int K, void* stream);
+/* Two such products sharing B in one launch: C0 = A0 B, C1 = A1 B (A0, A1 [M,K] with one lda; C0, C1
+ * [M,N] with one ldc).  The fold of W and V against the same embedding E (count_pipnet_utils.py:
+ * 378-385) as one grid of 2 x ceil(M/128) x ceil(N/128) tiles. */
+int pipnet_matmul2_f64acc_f32(const float* A0, const float* A1, int64_t lda, const float* B, int64_t ldb,
+                              float* C0, float* C1, int64_t ldc, int M, int N, int K, void* stream);
 
 /* ---- ResNet training step (csrc/bn_ops.hip): BatchNorm2d in train mode ------------------
  * Replaces the autograd of nn.BatchNorm2d(C) under net.train() in the ResNet Bottleneck /

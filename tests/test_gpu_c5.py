@@ -116,10 +116,10 @@ def test_c5_images_vs_oracle(c5):
 
 def test_matmul_f64acc_matches_float64(gpu):
     """pipnet_matmul_f64acc_f32 (csrc/fold_f64.hip) = float64 matmul rounded to fp32, on ragged
-    shapes (no multiple of the 64 x 64 x 16 tile) and on the C5 fold's own shape."""
+    shapes (no multiple of the 128 x 128 x 16 tile, odd K, N % 4 != 0) and on the C5 fold's own shape."""
     from count_pipnet_amd import kernels as K
     g = torch.Generator().manual_seed(7)
-    for m, n, k in [(1, 1, 1), (37, 70, 19), (130, 65, 257), (6144, 2048, 6144)]:
+    for m, n, k in [(1, 1, 1), (37, 70, 19), (130, 65, 257), (129, 131, 33), (256, 258, 18), (6144, 2048, 6144)]:
         a = torch.randn(m, k, generator=g)
         b = torch.randn(k, n, generator=g)
         ref = (a.double() @ b.double()).float()
@@ -128,6 +128,18 @@ def test_matmul_f64acc_matches_float64(gpu):
         ulp = torch.finfo(torch.float32).eps * ref.abs().clamp_min(1e-30)
         assert ((out - ref).abs() <= ulp).all(), (m, n, k)
         assert (out == ref).float().mean() > 0.999, (m, n, k)
+
+
+def test_matmul2_f64acc_pair_equals_singles(gpu):
+    """The one-launch pair form (W E, V E sharing E) is bitwise the two single products, ragged
+    and full-size, and leaves nothing outside its outputs."""
+    from count_pipnet_amd import kernels as K
+    g = torch.Generator().manual_seed(11)
+    for m, n, k in [(37, 70, 19), (300, 260, 100), (6144, 2048, 6144)]:
+        a0, a1 = torch.randn(m, k, generator=g).to(gpu), torch.randn(m, k, generator=g).to(gpu)
+        b = torch.randn(k, n, generator=g).to(gpu)
+        c0, c1 = K.matmul2_f64acc(a0, a1, b)
+        assert torch.equal(c0, K.matmul_f64acc(a0, b)) and torch.equal(c1, K.matmul_f64acc(a1, b)), (m, n, k)
 
 
 def test_bilinear_fold_tracks_weight_updates(gpu):
