@@ -18,9 +18,14 @@ int num_cus() {
   return 256;
 }
 
+// Raster group (tile_coords): group_m M-tiles are walked before N advances; budget in bytes of
+// 128-row A panels (build-time knob for tools/ab_build.py experiments)
+#ifndef PIPNET_BF16_GROUP_BUDGET
+#define PIPNET_BF16_GROUP_BUDGET (2.0 * 1024 * 1024)
+#endif
 int choose_group_m(int K) {
   const double panel = 128.0 * K * 2.0;
-  int g = (int)(2.0 * 1024 * 1024 / panel);
+  int g = (int)(PIPNET_BF16_GROUP_BUDGET / panel);
   return g < 1 ? 1 : (g > 16 ? 16 : g);
 }
 

@@ -25,6 +25,8 @@ for s in $STEPS; do
     bench) timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; stop_if_fatal $? bench; tail -3 gpurun_out/bench.log ;;
     prof)  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/prof.log" 2>&1); stop_if_fatal $? prof; find gpurun_out/prof -name "*stats*" | head ;;
     pmc)   timeout -k 10 900 bash tools/pmc.sh > gpurun_out/pmc.log 2>&1; stop_if_fatal $? pmc; tail -25 gpurun_out/pmc.log ;;
+    fold)  timeout -k 10 180 python tools/fold_bench.py > gpurun_out/fold_bench.txt 2>&1; stop_if_fatal $? fold; tail -1 gpurun_out/fold_bench.txt ;;
+    bf16lab) LAB_ABL=${LAB_ABL:-0,2,32,34,-1} LAB_SHAPES=${LAB_SHAPES:-sq4096,sq8192,l3c1,l4c1,l4ds,l3c3} timeout -k 10 600 python tools/bf16_lab.py > gpurun_out/bf16_lab.log 2>&1; stop_if_fatal $? bf16lab; grep -v "^\[\|amdgpu.ids" gpurun_out/bf16_lab.log | tail -20 ;;
   esac
 done
 exit 0
