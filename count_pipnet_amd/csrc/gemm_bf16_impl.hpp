@@ -25,6 +25,35 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+// Epilogue element math shared by the bf16 tiles (bitwise the element-wise forms they replace):
+// * add_bf16x8: the residual's 8 bf16 widened exactly to fp32 (a shift / mask per element) as two
+//   float4, so the adds issue as v_pk_add_f32 (one per 2 elements) instead of per-element v_add_f32;
+// * to_bf16x8: RNE to bf16 (v_cvt_pk_bf16_f32), then ReLU as v_pk_max_i16 against 0 on the packed
+//   pairs -- a bf16's bits order like an int16 (sign first), so max(bits, 0) zeroes exactly the
+//   negative values (-0 included) and keeps the rest: RNE(max(x, 0)) for every non-NaN x in one
+//   instruction per 2 elements instead of a v_max_f32 per element (a NaN now stays NaN, as torch's
+//   relu keeps it).
+PIPNET_DEV void add_bf16x8(f32x4& x0, f32x4& x1, const bf16x8& r) {
+  const u32x4 u = __builtin_bit_cast(u32x4, r);
+  const u32x4 ev = u << 16, od = u & 0xffff0000u;   // elements 2j (low half) / 2j + 1 (high half)
+  x0 += f32x4{__uint_as_float(ev[0]), __uint_as_float(od[0]), __uint_as_float(ev[1]), __uint_as_float(od[1])};
+  x1 += f32x4{__uint_as_float(ev[2]), __uint_as_float(od[2]), __uint_as_float(ev[3]), __uint_as_float(od[3])};
+}
+template <bool RELU>
+PIPNET_DEV unsigned bf16_pair(float a, float b) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  typedef short i16x2 __attribute__((ext_vector_type(2)));
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  i16x2 v = __builtin_bit_cast(i16x2, __builtin_convertvector((f32x2){a, b}, bf16x2));
+  if constexpr (RELU) v = __builtin_elementwise_max(v, (i16x2)0);
+  return __builtin_bit_cast(unsigned, v);
+}
+template <bool RELU>
+PIPNET_DEV bf16x8 to_bf16x8(const f32x4& x0, const f32x4& x1) {
+  return __builtin_bit_cast(bf16x8, u32x4{bf16_pair<RELU>(x0[0], x0[1]), bf16_pair<RELU>(x0[2], x0[3]),
+                                          bf16_pair<RELU>(x1[0], x1[1]), bf16_pair<RELU>(x1[2], x1[3])});
+}
+
 constexpr int KPAD = 64;                      // packed weights: K rounded up to this
 
 struct ConvParams {
@@ -271,26 +300,8 @@ PIPNET_DEV void epilogue(const ConvParams& p, const Acc<C>& acc, float* smem, in
         if (m < p.M && nok) finish_s3<EPI>(p, m, n, x0, x1, s0, s1);
         continue;
       }
-      if (HAS_R) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] += (float)r[i][it][e];
-          x1[e] += (float)r[i][it][4 + e];
-        }
-      }
-      if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] = fmaxf(x0[e], 0.f);
-          x1[e] = fmaxf(x1[e], 0.f);
-        }
-      }
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (bf16)x0[e];
-        o[4 + e] = (bf16)x1[e];
-      }
+      if (HAS_R) add_bf16x8(x0, x1, r[i][it]);
+      const bf16x8 o = to_bf16x8<EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU>(x0, x1);
       if (m < p.M && nok) *reinterpret_cast<bf16x8*>(p.C + (int64_t)m * p.ldc + n) = o;
     }
   }
@@ -442,6 +453,7 @@ __global__ __launch_bounds__(C::NTHREADS, MINB) void conv_bf16_kernel(ConvParams
 typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 
+
 namespace pp {
 constexpr int BM = 256, BN = 256, BK = 32, NT = 512;
 constexpr int ROWB = BK * 2;                          // 64 B per LDS row
@@ -549,26 +561,8 @@ PIPNET_DEV void pp_epilogue(const ConvParams& p, const f32x4v (&acc)[8][NB], uns
         if (m < p.M && nok) finish_s3<EPI>(p, m, n, x0, x1, s0, s1);
         continue;
       }
-      if (HAS_R) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] += (float)rr[it][e];
-          x1[e] += (float)rr[it][4 + e];
-        }
-      }
-      if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] = fmaxf(x0[e], 0.f);
-          x1[e] = fmaxf(x1[e], 0.f);
-        }
-      }
-      bf16x8v o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (bf16)x0[e];
-        o[4 + e] = (bf16)x1[e];
-      }
+      if (HAS_R) add_bf16x8(x0, x1, rr[it]);
+      const bf16x8v o = to_bf16x8<EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU>(x0, x1);
       if (m < p.M && nok) *reinterpret_cast<bf16x8v*>(op) = o;
       op += 8 * p.ldc;
     }
@@ -1013,26 +1007,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
         f32x4v x1 = *reinterpret_cast<const f32x4v*>(wt + row * 64 + ((8 * c8 + 4) ^ sw));
         x0 += b0;
         x1 += b1;
-        if (HAS_R) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x0[e] += (float)rr[r * 2 + it][e];
-            x1[e] += (float)rr[r * 2 + it][4 + e];
-          }
-        }
-        if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU || second) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            x0[e] = fmaxf(x0[e], 0.f);
-            x1[e] = fmaxf(x1[e], 0.f);
-          }
-        }
-        bf16x8v o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = (bf16)x0[e];
-          o[4 + e] = (bf16)x1[e];
-        }
+        if (HAS_R) add_bf16x8(x0, x1, rr[r * 2 + it]);
+        constexpr bool RELU = EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU;
+        const bf16x8v o = (RELU || second) ? to_bf16x8<true>(x0, x1) : to_bf16x8<false>(x0, x1);
         bf16* dst = mrow0 + 16 * r + 8 * it < p.M ? op : olast;     // row = it * 8 + (lane >> 3)
         __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(dst));
         op += 8 * ldo;
@@ -1466,26 +1443,9 @@ __global__ __launch_bounds__(hsm::NT, 2) void conv3x3_bf16_hsmall_kernel(ConvPar
       x0 += b0;
       x1 += b1;
       if (EPI == PIPNET_EPI_BIAS_RESID_RELU && m < p.M) {
-        const bf16x8 r = *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + 64 * wn + 8 * c8);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] += (float)r[e];
-          x1[e] += (float)r[4 + e];
-        }
+        add_bf16x8(x0, x1, *reinterpret_cast<const bf16x8*>(p.R + (int64_t)m * p.ldr + 64 * wn + 8 * c8));
       }
-      if (EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          x0[e] = fmaxf(x0[e], 0.f);
-          x1[e] = fmaxf(x1[e], 0.f);
-        }
-      }
-      bf16x8 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        o[e] = (bf16)x0[e];
-        o[4 + e] = (bf16)x1[e];
-      }
+      const bf16x8 o = to_bf16x8<EPI == PIPNET_EPI_BIAS_RELU || EPI == PIPNET_EPI_BIAS_RESID_RELU>(x0, x1);
       if (m < p.M) *reinterpret_cast<bf16x8*>(p.C + (int64_t)m * p.ldc + 64 * wn + 8 * c8) = o;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next block's writes
