@@ -61,8 +61,11 @@ struct MlpGeo {
 // (A staggered-halves form -- the second wave of each SIMD pair one chunk period late, so the two
 // waves' GELUs do not coincide -- was bitwise equal and no faster on any C2 / C5 shape in round 4;
 // profiles/r04/mlp_stagger_lab.txt.)
+// Launch bounds: at least 2 waves per SIMD for every workgroup size (MINB = 8 / NW workgroups per
+// CU), so the register allocation stays within 256 -- with the plain 256-thread bound hipcc spread
+// the C = 192 kernels over 198 VGPRs + 70 AGPRs, one wave per SIMD.
 template <int C, int HC, int NW, int PX, int HS = 1>
-__global__ __launch_bounds__(64 * NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
+__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
                                                               const float* __restrict__ W2,
                                                               const float* __restrict__ b2,
@@ -282,17 +285,24 @@ extern "C" int pipnet_cnblock_mlp_hw_f32(const float* t, const float* W1, const 
 #ifdef PIPNET_MLP_LAB
   if (pipnet_mlp_lab_variant(C, t, W1, b1, W2, b2, gamma, x, (int)M, s)) return PIPNET_OK;
 #endif
-  // small M (C1: 16 images of 64^2) gets smaller workgroups so that the grid still covers the CUs
+  // Workgroup shapes per M (tools/mlp_lab.py, profiles/r05/mlp_lab.txt; round 5 retuned the
+  // two-stream half batches of C2): C = 96 takes 4-wave workgroups from 98,304 pixels (C2 stage 1:
+  // 100,352 px 165.9 -> 150.7 us, 200,704 px 285.9 -> 273.8) and 8-wave ones at C5's 65,536
+  // (89.3 vs 93.3); C = 192 takes HC = 16 chunks at every M >= 8192 -- the HC = 32 chunks need
+  // 101 KiB of LDS, one 4-wave workgroup (one wave per SIMD) per CU: C2's 25,088-pixel stage-2
+  // half batch 198.6 -> 162.2 us on (16, 8), C5-sized 16,384 px 101.6 -> 99.4 on (16, 4).  Small M
+  // (C1: 16 images of 64^2) gets smaller workgroups so that the grid still covers the CUs.
   const int m = (int)M;
   if (C == 96) {
-    if (m >= 65536) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C2 / C5 stage 1
+    if (m >= 98304) return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C2 stage 1
+    if (m >= 65536) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C5 stage 1
     if (m >= 16384) return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
     if (m >= 8192) return launch_mlp<96, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
     return launch_mlp<96, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   }
   if (hw > 0 && hw <= MLP_HS2_MAX_HW) return launch_mlp<192, 16, 8, 1, 2>(t, W1, b1, W2, b2, gamma, x, m, s);  // C5 stage 2
-  if (m >= 32768) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);      // C2 stage 2
-  if (m >= 8192) return launch_mlp<192, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+  if (m >= 24576) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);      // C2 stage 2
+  if (m >= 8192) return launch_mlp<192, 16, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   if (m >= 4096) return launch_mlp<192, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
   return launch_mlp<192, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
 }

@@ -475,16 +475,23 @@ MLP_FUSED_CHANNELS = (96, 192)
 MLP_HS2_MAX_HW = 256    # C = 192 on maps of <= 16 x 16: hidden split over two waves (csrc/mlp_f32.hip)
 
 
+# pipnet_cnblock_mlp_hw_f32 thresholds (csrc/mlp_f32.hip, round 5: profiles/r05/mlp_lab.txt)
+MLP_C96_NW4_MIN_M = 98304
+MLP_C192_NW8_MIN_M = 24576
+
+
 def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20, hw: int = 0) -> str:
     """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32)."""
     if c == 192 and 0 < hw <= MLP_HS2_MAX_HW:
         return "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
     if c == 96:
-        nw = 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
+        nw = 4 if m >= MLP_C96_NW4_MIN_M else 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
         return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
-    if m >= 32768:
+    if m >= MLP_C192_NW8_MIN_M:
         return "cnblock_mlp_kernel<192, 16, 8, 1, 1>"
-    nw = 4 if m >= 8192 else 2 if m >= 4096 else 1
+    if m >= 8192:
+        return "cnblock_mlp_kernel<192, 16, 4, 1, 1>"
+    nw = 2 if m >= 4096 else 1
     return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
 
 

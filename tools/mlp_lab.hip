@@ -14,7 +14,8 @@ bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float*
   case ID: if (C != CC) return false; launch_mlp<CC, HC, NW, PX, HS>(t, W1, b1, W2, b2, gamma, x, M, s); return true;
   switch (g_variant) {
     V(1, 96, 32, 8, 2) V(2, 96, 32, 4, 2) V(4, 96, 32, 4, 1) V(5, 96, 16, 4, 2)
-    V(11, 192, 32, 8, 1) V(12, 192, 32, 4, 1) V(13, 192, 16, 8, 1) V(14, 192, 16, 2, 1)
+    V(11, 192, 32, 8, 1) V(12, 192, 32, 4, 1) V(13, 192, 16, 8, 1) V(14, 192, 16, 2, 1) V(15, 192, 16, 4, 1)
+    V(7, 96, 32, 2, 1)
     // hidden split over 2 waves per pixel group (HS = 2)
     V2(21, 192, 16, 8, 1, 2) V2(24, 192, 16, 4, 1, 2) V2(25, 192, 16, 2, 1, 2)
     V2(31, 96, 32, 8, 1, 2) V2(32, 96, 16, 8, 1, 2) V2(33, 96, 32, 4, 1, 2)

@@ -41,7 +41,10 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     g = torch.Generator(device=dev).manual_seed(0)
     rounds = int(os.environ.get("LAB_ROUNDS", "5"))
-    for c, m in [(96, 64 * 56 * 56), (192, 64 * 28 * 28), (96, 64 * 32 * 32), (192, 64 * 16 * 16)]:
+    shapes = [(96, 64 * 56 * 56), (192, 64 * 28 * 28), (96, 64 * 32 * 32), (192, 64 * 16 * 16)]
+    if os.environ.get("LAB_SHAPES"):      # e.g. "96x100352,192x25088" (C x M): the two-stream half batches
+        shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["LAB_SHAPES"].split(",")]
+    for c, m in shapes:
         t = torch.randn(m, c, device=dev, generator=g)
         x0 = torch.randn(m, c, device=dev, generator=g)
         w1 = torch.randn(4 * c, c, device=dev, generator=g) * 0.1
