@@ -24,10 +24,16 @@ int choose_group_m(const GemmParams& p) {
 //   otherwise                 BK=32, 128-row tiles, 2 LDS stages      (stage-3/4 fc1, fc2)
 // 0 = register-staged K-tail kernel, 1 = BK16x128 rows x3 stages, 2 = BK32x64 rows,
 // 3 = BK32x128 rows (mirrored by count_pipnet_amd/kernels.py:gemm_kernel_name)
+// (PIPNET_AB_GEMM_RULE: build-time A/B hook for tools/ab_build.py, 0 in the product)
+#ifndef PIPNET_AB_GEMM_RULE
+#define PIPNET_AB_GEMM_RULE 0
+#endif
 int gemm_variant(int M, int N, int K, bool vec) {
   if (!vec) return 0;
   if (K % 16 == 0 && K <= 96 && N > 192 && M > 64) return 1;
   if (K % 32) return K % 16 == 0 && M > 64 ? 1 : 0;
+  if (PIPNET_AB_GEMM_RULE == 1 && N == 384 && K >= 1536 && M > 64) return 3;   // stage-3 fc2 on 128-row tiles
+  if (PIPNET_AB_GEMM_RULE == 2 && N == 1536 && K == 384) return 2;              // stage-3 fc1 on 64-row tiles
   if (N <= 384 || K <= 192 || M <= 64) return 2;
   return 3;
 }
