@@ -59,8 +59,9 @@ SIGNATURES = {
     "pipnet_dwconv7_ln_f32": [P, I32, I32, I32, I32, P, P, P, P, P, P],
     "pipnet_layernorm_f32": [P, I64, I32, P, P, P, P],
     "pipnet_softmax_pool_f32": [P, I32, I32, I32, I32, P, P, P],
-    "pipnet_softmax_pool_linear_f32": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P],
-    "pipnet_softmax_pool_linear_bf16": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P],
+    "pipnet_softmax_pool_linear_part_floats": [I32, I32, I32],
+    "pipnet_softmax_pool_linear_f32": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P, P],
+    "pipnet_softmax_pool_linear_bf16": [P, I32, I32, I32, P, P, P, P, I32, I32, F32, P, P, P, P, P],
     "pipnet_nonneg_linear_f32": [P, I32, I32, P, P, I32, I32, F32, P, P, P],
     "pipnet_count_gumbel_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_count_gumbel_devseed_f32": [P, I32, I32, I32, F32, P, P, P, P],
@@ -97,7 +98,8 @@ SIGNATURES = {
     "pipnet_stride_scatter_f32": [P, I32, I32, I32, I32, I32, I32, I32, I32, P, P],
 }
 _RESTYPE_EXTRA = {"pipnet_wgrad_workspace_bytes": ctypes.c_int64, "pipnet_train_partials_floats": ctypes.c_int64,
-                  "pipnet_bn_workspace_floats": ctypes.c_int64}
+                  "pipnet_bn_workspace_floats": ctypes.c_int64,
+                  "pipnet_softmax_pool_linear_part_floats": ctypes.c_int64}
 _RESTYPE = {"pipnet_amd_status_string": ctypes.c_char_p, "pipnet_amd_source_digest": ctypes.c_char_p,
             **_RESTYPE_EXTRA}
 

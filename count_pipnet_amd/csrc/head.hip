@@ -38,20 +38,20 @@ constexpr int HEAD_THREADS = 256;
 constexpr int PIX_PER_BLOCK = 32;
 
 // ---------------------------------------------------------------------------------------
-// NonNegLinear (pipnet.py:36-37, 54-71) fused into the softmax-pool head: the classifier of
-// image b runs in the LAST workgroup of b's pixel blocks, chosen by an arrival ticket.
-//   * every workgroup's atomicMax of its pixel-block maxima into pooled[b] is acknowledged
-//     (vmcnt(0): a no-return atomic stays counted until performed at the memory side) before
-//     its thread 0 takes a ticket (atomicAdd on tickets[b], also performed there);
-//   * the workgroup that draws gridDim.x - 1 reads pooled[b] back through atomic RMWs
-//     (atomicOr 0: served at the memory side, so no XCD's stale L2 / L1 copy is read),
-//     applies the 0.1 presence threshold in inference mode, writes the clamped row (x_out)
-//     and runs the GEMV x' relu(W)^T + bias against W as it is at call time;
-//   * the GEMV keeps nonneg_linear_kernel's arithmetic exactly (per-thread float4 slices,
-//     16 class partials, fmaf order, wave then cross-wave sums), so the fused head is bitwise
-//     the two-kernel path.
-// Tickets are zeroed by the same zero-fill launch as pooled.
-// ---------------------------------------------------------------------------------------
+// NonNegLinear (pipnet.py:36-37, 54-71) fused into the softmax-pool head -- the whole head is ONE
+// launch (no zero-fill of pooled or of the tickets ahead of it):
+//   * every workgroup stores its pixel block's per-channel maxima into its own slot of a partial
+//     buffer (plain stores), publishes them (vmcnt(0), workgroup barrier, one agent-scope release
+//     fence) and takes an arrival ticket for its image (relaxed agent-scope fetch_add);
+//   * the workgroup that draws gridDim.x - 1 acquires (agent-scope fence), takes the max over the
+//     image's partial slots (max is exact in any order), writes pooled[b], applies the 0.1 presence
+//     threshold in inference mode, writes the clamped row (x_out), runs the GEMV x' relu(W)^T +
+//     bias against W as it is at call time, and resets its ticket to 0 -- so the ticket words
+//     are zero again after every completed call (the caller zeroes them once, at allocation);
+//   * the GEMV keeps nonneg_linear_kernel's arithmetic exactly (per-thread float4 slices, 16
+//     class partials, fmaf order, wave then cross-wave sums), so the fused head is bitwise the
+//     two-kernel path.
+// (cdna_hip_programming.md, "In-launch split-K reduction": release/acquire once per episode.)
 constexpr int NN_CLS_PER_BLOCK = 16;
 
 struct HeadLinear {
@@ -62,8 +62,12 @@ struct HeadLinear {
   float thresh;
   float* x_out;          // [B, P] clamped (or copied) pooled row, or null
   float* out;            // [B, K] logits
-  int32_t* tickets;      // [B] arrival tickets (zeroed with pooled)
+  int32_t* tickets;      // [B] arrival tickets: zero on entry, zero again on exit
+  float* part;           // [B, gridDim.x, P] per-pixel-block maxima
 };
+
+// partial maxima: one P-row per (image, pixel block)
+inline int64_t head_part_floats(int B, int HW, int P) { return (int64_t)B * ((HW + 31) / 32) * P; }
 
 // One row of NonNegLinear: x (P floats, any address space the caller owns) -> out[0..K).
 // Called by all HEAD_THREADS threads of a workgroup; red = [4][16] floats of LDS.
@@ -115,25 +119,39 @@ PIPNET_DEV void nonneg_linear_row(const float* x, int D, const float* __restrict
   }
 }
 
-// The fused head's tail (after the workgroup's atomicMax loop).  xs = >= P floats of LDS the
-// workgroup no longer needs.
+// The fused head's tail, called after the workgroup stored its block maxima into hl.part.
+// xs = >= P floats of LDS the workgroup no longer needs.
 PIPNET_DEV void head_linear_tail(const HeadLinear& hl, int b, int P, float* pooled, float* xs) {
   __shared__ int is_last;
   __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
-  vm_drain();                                  // this thread's atomicMax ops performed
+  vm_drain();                                  // this thread's partial stores performed
   __syncthreads();
-  if (threadIdx.x == 0) is_last = atomicAdd(hl.tickets + b, 1) == (int)gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    vm_drain();
+    is_last = __hip_atomic_fetch_add(hl.tickets + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              (int)gridDim.x - 1;
+  }
   __syncthreads();
   if (!is_last) return;
-  unsigned* prow = reinterpret_cast<unsigned*>(pooled + (int64_t)b * P);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    vm_drain();
+  }
+  __syncthreads();
+  const int nblk = gridDim.x;
+  const float* prt = hl.part + (int64_t)b * nblk * P;
   for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
-    float v = __uint_as_float(atomicOr(prow + c, 0u));
+    float v = prt[c];
+    for (int k = 1; k < nblk; ++k) v = fmaxf(v, prt[(int64_t)k * P + c]);
+    pooled[(int64_t)b * P + c] = v;
     if (hl.apply_thresh && v < hl.thresh) v = 0.f;
     xs[c] = v;
     if (hl.x_out) hl.x_out[(int64_t)b * P + c] = v;
   }
   __syncthreads();
   nonneg_linear_row(xs, P, hl.W, hl.bias, hl.K, hl.out + (int64_t)b * hl.K, red);
+  if (threadIdx.x == 0) hl.tickets[b] = 0;    // every workgroup of b has drawn: ready for the next call
 }
 
 // ---------------------------------------------------------------------------------------
@@ -188,12 +206,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
 #pragma unroll
     for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
     float* dst = pooled + (int64_t)b * P + c;
-    if (MODE == 0)   // non-negative floats order like their bit patterns
+    if (LIN)         // this block's maxima, reduced by the image's last workgroup
+      hl.part[((int64_t)b * gridDim.x + blockIdx.x) * P + c] = r;
+    else if (MODE == 0)   // non-negative floats order like their bit patterns
       atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
     else
       atomicAdd(dst, r);
   }
-  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);
+  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
 }
 
 // bf16 logits (the C3 ResNet build, P = 2048), quad layout (round 4): lane l holds channels
@@ -280,12 +300,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
 #pragma unroll
     for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
     float* dst = pooled + (int64_t)b * P + c;
-    if (MODE == 0)
+    if (LIN)         // this block's maxima, reduced by the image's last workgroup
+      hl.part[((int64_t)b * gridDim.x + blockIdx.x) * P + c] = r;
+    else if (MODE == 0)   // non-negative floats order like their bit patterns
       atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
     else
       atomicAdd(dst, r);
   }
-  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);
+  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
 }
 
 // ---------------------------------------------------------------------------------------
@@ -623,13 +645,13 @@ int head_launch(const T* feat, int B, int HW, int P, int pool_mode, float* proto
   const bool lin = hl.W != nullptr;
   if (B < 0 || HW <= 0 || P <= 0 || (pool_mode != 0 && pool_mode != 1) || (lin && pool_mode != 0)) return PIPNET_ERR_ARG;
   if (!feat || !proto || !pooled) return PIPNET_ERR_ARG;
-  if (lin && (hl.K <= 0 || !hl.out || !hl.tickets)) return PIPNET_ERR_ARG;
+  if (lin && (hl.K <= 0 || !hl.out || !hl.tickets || !hl.part)) return PIPNET_ERR_ARG;
   if (lin && (P & 3) == 0 && !aligned16(hl.W)) return PIPNET_ERR_ALIGN;
   if (B == 0) return PIPNET_OK;
   const int nj = nj_bucket(P);
   if (nj < 0) return PIPNET_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
-  if (!zero_fill(pooled, (int64_t)B * P, s, lin ? hl.tickets : nullptr, B)) return PIPNET_ERR_LAUNCH;
+  if (!lin && !zero_fill(pooled, (int64_t)B * P, s)) return PIPNET_ERR_LAUNCH;   // the fused head needs none
   const dim3 grid((HW + PIX_PER_BLOCK - 1) / PIX_PER_BLOCK, B);
   const dim3 block(HEAD_THREADS);
   constexpr bool BF = std::is_same<T, __bf16>::value;
@@ -671,20 +693,24 @@ extern "C" int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, 
 
 extern "C" int pipnet_softmax_pool_linear_f32(const float* feat, int B, int HW, int P, float* proto, float* pooled,
                                               const float* W, const float* bias, int K, int apply_thresh,
-                                              float thresh, float* x_out, float* out, int32_t* tickets,
-                                              void* stream) {
+                                              float thresh, float* x_out, float* out, float* part,
+                                              int32_t* tickets, void* stream) {
   if (!W) return PIPNET_ERR_ARG;
-  return head_launch(feat, B, HW, P, 0, proto, pooled, HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets},
-                     stream);
+  return head_launch(feat, B, HW, P, 0, proto, pooled,
+                     HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets, part}, stream);
 }
 
 extern "C" int pipnet_softmax_pool_linear_bf16(const void* feat, int B, int HW, int P, float* proto, float* pooled,
                                                const float* W, const float* bias, int K, int apply_thresh,
-                                               float thresh, float* x_out, float* out, int32_t* tickets,
-                                               void* stream) {
+                                               float thresh, float* x_out, float* out, float* part,
+                                               int32_t* tickets, void* stream) {
   if (!W) return PIPNET_ERR_ARG;
   return head_launch(reinterpret_cast<const __bf16*>(feat), B, HW, P, 0, proto, pooled,
-                     HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets}, stream);
+                     HeadLinear{W, bias, K, apply_thresh, thresh, x_out, out, tickets, part}, stream);
+}
+
+extern "C" int64_t pipnet_softmax_pool_linear_part_floats(int B, int HW, int P) {
+  return (B < 0 || HW <= 0 || P <= 0) ? 0 : head_part_floats(B, HW, P);
 }
 
 extern "C" int pipnet_nonneg_linear_f32(const float* x, int B, int D, const float* W, const float* bias, int K,

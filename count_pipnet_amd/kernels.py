@@ -656,12 +656,34 @@ def softmax_pool_linear(feat_nhwc: Tensor, w: Tensor, bias: Optional[Tensor], th
             raise RuntimeError("softmax_pool_linear: out shapes do not match")
         _chk(x_out, "classifier input out")
         _chk(logits, "logits out")
-    tickets = torch.empty((b,), device=dev, dtype=torch.int32)       # zeroed by the launch
+    part, tickets = _head_workspace(dev, _stream(feat_nhwc), int(_lib.load().pipnet_softmax_pool_linear_part_floats(
+        b, h * wd, p)), b)
     _lib.call("pipnet_softmax_pool_linear_bf16" if bf else "pipnet_softmax_pool_linear_f32", feat_nhwc.data_ptr(), b,
               h * wd, p, proto.data_ptr(), pooled.data_ptr(), w.data_ptr(), _ptr(bias), k,
               0 if thresh is None else 1, 0.0 if thresh is None else float(thresh), x_out.data_ptr(),
-              logits.data_ptr(), tickets.data_ptr(), _stream(feat_nhwc))
+              logits.data_ptr(), part.data_ptr(), tickets.data_ptr(), _stream(feat_nhwc))
     return proto, pooled, x_out, logits
+
+
+# Fused-head scratch, one (partials, tickets) pair per (device, stream): the tickets are zeroed once
+# here, in a buffer of their own, and left zero by every completed launch (include/pipnet_amd.h), so
+# the head needs no memset per call; per stream because two concurrent heads (the split forward's
+# sub-batch streams) must not share them.  Buffers only grow; a grown one is allocated (zeroed) on
+# the stream that uses it.
+_HEAD_WS = {}
+
+
+def _head_workspace(dev: torch.device, stream: int, nfloats: int, b: int) -> Tuple[Tensor, Tensor]:
+    key = (dev.index, stream)
+    part, tickets = _HEAD_WS.get(key, (None, None))
+    capturing = torch.cuda.is_current_stream_capturing()
+    if part is None or part.numel() < nfloats:
+        part = torch.empty(max(nfloats, 4), device=dev, dtype=torch.float32)
+    if tickets is None or tickets.numel() < b:
+        tickets = torch.zeros(max(b, 64), device=dev, dtype=torch.int32)
+    if not capturing:          # graph-owned buffers (their zero-fill replays with them) are never cached
+        _HEAD_WS[key] = (part, tickets)
+    return part, tickets
 
 
 def nonneg_linear(x: Tensor, w: Tensor, bias: Optional[Tensor], thresh: Optional[float],

@@ -51,8 +51,8 @@ extern "C" {
  * its `pad` argument (round 2).  3: the process-wide A/B switches (pipnet_gemm_persist /
  * _stream / _bk16x3 / _plain_store, pipnet_conv_bf16_rb, pipnet_head_bf16_quads) and
  * pipnet_linear_agelu_f32 are gone -- kernel selection is a fixed per-shape rule with no
- * mutable library state -- and the fused head pipnet_softmax_pool_linear_f32 / _bf16 is new
- * (round 5).  A caller built against an older version must not bind this library. */
+ * mutable library state -- and the one-launch fused head pipnet_softmax_pool_linear_f32 / _bf16
+ * (+ _part_floats) and pipnet_matmul2_f64acc_f32 are new (round 5).  A caller built against an older version must not bind this library. */
 #define PIPNET_AMD_ABI_VERSION 3
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -226,14 +226,20 @@ int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mo
  * once, spatial max into pooled [B,P], then -- in the last workgroup to finish image b (an
  * arrival ticket) -- x' = where(pooled < thresh, 0, pooled) when apply_thresh, else pooled,
  * written to x_out [B,P] (may be NULL), and out [B,K] = x' relu(W)^T + bias, W [K,P] read at
- * call time.  tickets: int32 [B] workspace (zeroed by this call together with pooled).  Bitwise
- * equal to the two-kernel path.  W 16-B aligned when P % 4 == 0.  _bf16: bf16 logits. */
+ * call time.  Bitwise equal to the two-kernel path.  W 16-B aligned when P % 4 == 0.  _bf16:
+ * bf16 logits.
+ * part: pipnet_softmax_pool_linear_part_floats(B, HW, P) floats of scratch (per-pixel-block
+ * maxima).  tickets: int32 [B] arrival counters that must be ZERO on entry -- zero them once at
+ * allocation: every completed call leaves tickets[0..B) zero again, so no memset is needed
+ * between calls.  Keep them in their own buffer (never let other data overwrite them) and give
+ * calls that may run concurrently (different streams) separate part / tickets buffers. */
+int64_t pipnet_softmax_pool_linear_part_floats(int B, int HW, int P);
 int pipnet_softmax_pool_linear_f32(const float* feat, int B, int HW, int P, float* proto, float* pooled,
                                    const float* W, const float* bias, int K, int apply_thresh, float thresh,
-                                   float* x_out, float* out, int32_t* tickets, void* stream);
+                                   float* x_out, float* out, float* part, int32_t* tickets, void* stream);
 int pipnet_softmax_pool_linear_bf16(const void* feat, int B, int HW, int P, float* proto, float* pooled,
                                     const float* W, const float* bias, int K, int apply_thresh, float thresh,
-                                    float* x_out, float* out, int32_t* tickets, void* stream);
+                                    float* x_out, float* out, float* part, int32_t* tickets, void* stream);
 
 /* ---- eval_pipnet metric loop (pipnet/test.py:67-131,266-319) -------
  * One evaluation batch, entirely on the device (no host sync):

@@ -425,10 +425,54 @@ def test_fused_head_bitwise_two_kernel_path(gpu, dtype, b, hw, p, k, thresh):
         xr = torch.where(xr < thresh, 0.0, xr)
     ref = xr @ w.double().clamp_min(0).t() + bias.double()
     assert (out.double() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
-    # a second call on reused (non-zero) buffers: tickets and pooled are re-zeroed by the launch
+    # a second call into reused (non-zero) output buffers and the same workspace, whose tickets
+    # the first call must have left at zero
     proto3, pooled3, xo3, out3 = K.softmax_pool_linear(f4, w, bias, thresh, out=(proto, pooled, xo, out.clone()))
     torch.cuda.synchronize()
     assert torch.equal(out3, out2) and torch.equal(pooled3, pooled2)
+    _, tickets = K._HEAD_WS[(f4.device.index, torch.cuda.current_stream(f4.device).cuda_stream)]
+    assert int(tickets.abs().sum().item()) == 0        # tickets reset by the launch
+
+
+def test_fused_head_is_one_launch(gpu):
+    """The PIP-Net head is a single kernel launch (no zero-fill of pooled or tickets ahead of it):
+    counted with the HIP-graph node count of a captured call."""
+    g = torch.Generator().manual_seed(5)
+    feat = (torch.randn(8, 2, 26, 768, generator=g) * 6).to(gpu)      # peaked softmax: presence > 0.1
+    w = torch.randn(200, 768, generator=g).to(gpu)
+    K.softmax_pool_linear(feat, w, None, 0.1)          # workspace allocated outside the capture
+    s = torch.cuda.Stream(gpu)
+    s.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(s):
+        K.softmax_pool_linear(feat, w, None, 0.1)      # this stream's workspace, outside the capture
+        outs = [torch.full((8, 2, 26, 768), -1.0, device=gpu), torch.full((8, 768), -1.0, device=gpu),
+                torch.full((8, 768), -1.0, device=gpu), torch.full((8, 200), -1.0, device=gpu)]
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(graph, stream=s):
+        K.softmax_pool_linear(feat, w, None, 0.1, out=tuple(outs))
+    torch.cuda.synchronize()
+    n = _graph_nodes(graph)
+    graph.instantiate()
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    ref = K.softmax_pool_linear(feat, w, None, 0.1)
+    torch.cuda.synchronize()
+    assert n == 1, n
+    assert ref[3].abs().sum().item() > 0
+    for name, a, r in zip(("proto", "pooled", "x'", "logits"), outs, ref):
+        assert torch.equal(a, r), (name, (a - r).abs().max().item())
+
+
+def _graph_nodes(graph) -> int:
+    """Number of nodes of a captured torch CUDAGraph(keep_graph=True) (hipGraphGetNodes)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    count = ctypes.c_size_t(0)
+    hip.hipGraphGetNodes.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+    assert hip.hipGraphGetNodes(ctypes.c_void_p(graph.raw_cuda_graph()), None, ctypes.byref(count)) == 0
+    return count.value
 
 
 def test_fused_head_reads_weight_at_call_time(gpu):
