@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 4 PMC passes (clock / MFMA busy, FETCH_SIZE, WRITE_SIZE; separate runs) over C2 (bench.py),
+# PMC passes (clock / MFMA busy, FETCH_SIZE, WRITE_SIZE; separate runs) over C2 (bench.py),
 # C3 and C5 (tools/bench_configs.py), one stream each.
 set -u
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$PWD
 export TMPDIR=/tmp
 mkdir -p gpurun_out

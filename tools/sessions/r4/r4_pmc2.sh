@@ -4,7 +4,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-bash tools/sessions/r4_pmc.sh || exit $?
+bash tools/pmc_all.sh || exit $?
 PMC_OUT=pmc_s3 PMC_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-extra --precision bf16x3 --alt-precision none --stream-split 1" \
   timeout -k 10 900 bash tools/pmc.sh > gpurun_out/pmc_s3.log 2>&1 || exit $?
 tail -6 gpurun_out/pmc_s3.log

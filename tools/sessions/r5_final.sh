@@ -9,7 +9,7 @@ R=$PWD
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ "${SKIP_PMC:-0}" != 1 ]; then
-  bash tools/sessions/r4_pmc.sh || exit $?
+  bash tools/pmc_all.sh || exit $?
   python3 - <<'PY' || exit $?
 import json, shutil
 shutil.copy("gpurun_out/pmc/traffic_latest.json", "profiles/traffic_latest.json")
