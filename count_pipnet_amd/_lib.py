@@ -28,6 +28,7 @@ SIGNATURES = {
     "pipnet_linear_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, P],
     "pipnet_linear_rowscale_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, P, I32, P],
     "pipnet_linear_splitk_f32": [P, I64, P, P, P, P, I64, P, I64, I32, I32, I32, I32, I32, P, P],
+    "pipnet_linear_pair_mul_f32": [P, I64, P, P, I64, I32, I32, I32, I32, P, P],
     "pipnet_matmul_f64acc_f32": [P, I64, P, I64, P, I64, I32, I32, I32, P],
     "pipnet_matmul2_f64acc_f32": [P, P, I64, P, I64, P, P, I64, I32, I32, I32, P],
     "pipnet_conv2x2_f32": [P, I32, I32, I32, I32, P, P, I32, I32, P, P],

@@ -57,6 +57,26 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float* __restr
   }
 }
 
+// split-K reduction of a paired GEMM (N = 2 Nh columns: [A W1^T | A W2^T]) with the pair multiplied:
+// C[m][n] = (sum_s slab_s[m][Nh + n]) * (sum_s slab_s[m][n]), n < Nh -- BilinearIntermediate's
+// W(e) * V(e) on the folded pair (count_pipnet_utils.py:378-385), the same product as the
+// EPI_MUL epilogue of the V GEMM with the W GEMM's output as R.
+__global__ __launch_bounds__(256) void splitk_pair_mul_kernel(const float* __restrict__ ws, int splits, int64_t slab,
+                                                              int M, int Nh, float* C, int64_t ldc) {
+  const int n4 = Nh / 4;
+  const int64_t total = (int64_t)M * n4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int m = (int)(i / n4), n = 4 * (int)(i - (int64_t)m * n4);
+    const float* r = ws + (int64_t)m * 2 * Nh + n;
+    f32x4 a = ld4(r), v = ld4(r + Nh);
+    for (int sp = 1; sp < splits; ++sp) {
+      a += ld4(r + sp * slab);
+      v += ld4(r + sp * slab + Nh);
+    }
+    st4(C + (int64_t)m * ldc + n, v * a);
+  }
+}
+
 // compute units of the current device (queried per launch: no process-wide cache, so every
 // device of a multi-GPU process gets its own answer; the runtime serves it from its device table)
 int num_cus() {
@@ -183,6 +203,32 @@ extern "C" int pipnet_conv2d_nhwc_f32(const float* x, int B, int H, int W, int C
     return launch_gemm<ALOAD_DENSE>(p, epilogue, (hipStream_t)stream);
   }
   return launch_gemm<ALOAD_CONV>(p, epilogue, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_linear_pair_mul_f32(const float* A, int64_t lda, const float* Wpair, float* C, int64_t ldc, int M,
+                                          int Nh, int K, int splits, float* workspace, void* stream) {
+  if (M < 0 || Nh <= 0 || K <= 0 || (Nh & 3) || (K % 32) || (lda & 3) || lda < K || (ldc & 3) || ldc < Nh)
+    return PIPNET_ERR_ARG;
+  if (splits < 1 || splits > K / 32 || splits > 64 || !workspace || !A || !Wpair || !C) return PIPNET_ERR_ARG;
+  if (!aligned16(A) || !aligned16(Wpair) || !aligned16(C) || !aligned16(workspace)) return PIPNET_ERR_ALIGN;
+  if (M == 0) return PIPNET_OK;
+  hipStream_t s = (hipStream_t)stream;
+  GemmParams p{};
+  p.A = A; p.lda = lda; p.W = Wpair; p.C = workspace; p.ldc = 2 * Nh; p.M = M; p.N = 2 * Nh; p.K = K;
+  p.nt = (p.N + BN - 1) / BN;
+  p.mt = (M + 63) / 64;
+  p.group_m = choose_group_m(p);
+  p.vec_epi = 1;
+  p.split_stride = (int64_t)M * p.N;
+  const dim3 grid(p.mt * p.nt, splits);
+  hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, PIPNET_EPI_NONE, ALOAD_DENSE, 3, 2>), grid, dim3(NTHREADS), 0, s, p);
+  PIPNET_CHECK_LAUNCH();
+  const int64_t work = (int64_t)M * (Nh / 4);
+  const int blocks = (int)((work + 255) / 256 < 4096 ? (work + 255) / 256 : 4096);
+  hipLaunchKernelGGL(splitk_pair_mul_kernel, dim3(blocks), dim3(256), 0, s, workspace, splits, p.split_stride, M, Nh, C,
+                     ldc);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
 }
 
 extern "C" int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float* W, const float* bias,

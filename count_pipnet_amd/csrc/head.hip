@@ -39,19 +39,22 @@ constexpr int PIX_PER_BLOCK = 32;
 
 // ---------------------------------------------------------------------------------------
 // NonNegLinear (pipnet.py:36-37, 54-71) fused into the softmax-pool head -- the whole head is ONE
-// launch (no zero-fill of pooled or of the tickets ahead of it):
-//   * every workgroup stores its pixel block's per-channel maxima into its own slot of a partial
-//     buffer (plain stores), publishes them (vmcnt(0), workgroup barrier, one agent-scope release
-//     fence) and takes an arrival ticket for its image (relaxed agent-scope fetch_add);
-//   * the workgroup that draws gridDim.x - 1 acquires (agent-scope fence), takes the max over the
-//     image's partial slots (max is exact in any order), writes pooled[b], applies the 0.1 presence
-//     threshold in inference mode, writes the clamped row (x_out), runs the GEMV x' relu(W)^T +
-//     bias against W as it is at call time, and resets its ticket to 0 -- so the ticket words
-//     are zero again after every completed call (the caller zeroes them once, at allocation);
+// launch (no zero-fill ahead of it):
+//   * every workgroup atomicMax-es its pixel block's per-channel maxima into a scratch row pmax[b]
+//     (memory-side atomics: non-negative floats order like their bit patterns) and, once they are
+//     acknowledged (vmcnt(0): a no-return atomic stays counted until performed at the memory side),
+//     takes an arrival ticket for its image (atomicAdd, also performed there);
+//   * the workgroup that draws gridDim.x - 1 takes the row back with atomicExch(.., 0) -- read at
+//     the memory side (no XCD's stale L2 copy) and reset in the same operation -- writes pooled[b],
+//     applies the 0.1 presence threshold in inference mode, writes the clamped row (x_out), runs the
+//     GEMV x' relu(W)^T + bias against W as it is at call time, and resets its ticket: scratch and
+//     tickets are zero again after every completed call (the caller zeroes them once);
+//   * no fences: a release fence per workgroup (partial-slab stores + agent-scope release /
+//     acquire, tried first in round 5) wrote back the L2 behind the streaming proto stores 3,200
+//     times per C3 call and tripled the head's time;
 //   * the GEMV keeps nonneg_linear_kernel's arithmetic exactly (per-thread float4 slices, 16
 //     class partials, fmaf order, wave then cross-wave sums), so the fused head is bitwise the
 //     two-kernel path.
-// (cdna_hip_programming.md, "In-launch split-K reduction": release/acquire once per episode.)
 constexpr int NN_CLS_PER_BLOCK = 16;
 
 struct HeadLinear {
@@ -63,11 +66,10 @@ struct HeadLinear {
   float* x_out;          // [B, P] clamped (or copied) pooled row, or null
   float* out;            // [B, K] logits
   int32_t* tickets;      // [B] arrival tickets: zero on entry, zero again on exit
-  float* part;           // [B, gridDim.x, P] per-pixel-block maxima
+  float* part;           // [B, P] running maxima (pmax): zero on entry, zero again on exit
 };
 
-// partial maxima: one P-row per (image, pixel block)
-inline int64_t head_part_floats(int B, int HW, int P) { return (int64_t)B * ((HW + 31) / 32) * P; }
+inline int64_t head_part_floats(int B, int HW, int P) { return HW > 0 ? (int64_t)B * P : 0; }
 
 // One row of NonNegLinear: x (P floats, any address space the caller owns) -> out[0..K).
 // Called by all HEAD_THREADS threads of a workgroup; red = [4][16] floats of LDS.
@@ -119,39 +121,27 @@ PIPNET_DEV void nonneg_linear_row(const float* x, int D, const float* __restrict
   }
 }
 
-// The fused head's tail, called after the workgroup stored its block maxima into hl.part.
-// xs = >= P floats of LDS the workgroup no longer needs.
+// The fused head's tail, called after the workgroup's atomicMax loop into hl.part.  xs = >= P
+// floats of LDS the workgroup no longer needs.
 PIPNET_DEV void head_linear_tail(const HeadLinear& hl, int b, int P, float* pooled, float* xs) {
   __shared__ int is_last;
   __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
-  vm_drain();                                  // this thread's partial stores performed
+  vm_drain();                                  // this thread's atomicMax ops performed
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    vm_drain();
-    is_last = __hip_atomic_fetch_add(hl.tickets + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              (int)gridDim.x - 1;
-  }
+  if (threadIdx.x == 0) is_last = atomicAdd(hl.tickets + b, 1) == (int)gridDim.x - 1;
   __syncthreads();
   if (!is_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    vm_drain();
-  }
-  __syncthreads();
-  const int nblk = gridDim.x;
-  const float* prt = hl.part + (int64_t)b * nblk * P;
+  unsigned* prow = reinterpret_cast<unsigned*>(hl.part + (int64_t)b * P);
   for (int c = threadIdx.x; c < P; c += HEAD_THREADS) {
-    float v = prt[c];
-    for (int k = 1; k < nblk; ++k) v = fmaxf(v, prt[(int64_t)k * P + c]);
+    float v = __uint_as_float(atomicExch(prow + c, 0u));   // read at the memory side, scratch reset
     pooled[(int64_t)b * P + c] = v;
     if (hl.apply_thresh && v < hl.thresh) v = 0.f;
     xs[c] = v;
     if (hl.x_out) hl.x_out[(int64_t)b * P + c] = v;
   }
   __syncthreads();
+  if (threadIdx.x == 0) atomicExch(hl.tickets + b, 0);   // every workgroup of b has drawn
   nonneg_linear_row(xs, P, hl.W, hl.bias, hl.K, hl.out + (int64_t)b * hl.K, red);
-  if (threadIdx.x == 0) hl.tickets[b] = 0;    // every workgroup of b has drawn: ready for the next call
 }
 
 // ---------------------------------------------------------------------------------------
@@ -205,10 +195,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
     float r = red[0][c];
 #pragma unroll
     for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
-    float* dst = pooled + (int64_t)b * P + c;
-    if (LIN)         // this block's maxima, reduced by the image's last workgroup
-      hl.part[((int64_t)b * gridDim.x + blockIdx.x) * P + c] = r;
-    else if (MODE == 0)   // non-negative floats order like their bit patterns
+    float* dst = (LIN ? hl.part : pooled) + (int64_t)b * P + c;   // LIN: the scratch row, read back by the last workgroup
+    if (MODE == 0)   // non-negative floats order like their bit patterns
       atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
     else
       atomicAdd(dst, r);
@@ -299,10 +287,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
     float r = red[0][c];
 #pragma unroll
     for (int w = 1; w < HEAD_THREADS / 64; ++w) r = MODE == 0 ? fmaxf(r, red[w][c]) : r + red[w][c];
-    float* dst = pooled + (int64_t)b * P + c;
-    if (LIN)         // this block's maxima, reduced by the image's last workgroup
-      hl.part[((int64_t)b * gridDim.x + blockIdx.x) * P + c] = r;
-    else if (MODE == 0)   // non-negative floats order like their bit patterns
+    float* dst = (LIN ? hl.part : pooled) + (int64_t)b * P + c;   // LIN: the scratch row, read back by the last workgroup
+    if (MODE == 0)   // non-negative floats order like their bit patterns
       atomicMax(reinterpret_cast<unsigned int*>(dst), __float_as_uint(r));
     else
       atomicAdd(dst, r);

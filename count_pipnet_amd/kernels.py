@@ -128,6 +128,26 @@ def linear(a: Tensor, w: Tensor, bias: Optional[Tensor] = None, epilogue: int = 
     return out
 
 
+def linear_pair_mul(a: Tensor, w_pair: Tensor) -> Tensor:
+    """(a @ w_pair[Nh:]^T) * (a @ w_pair[:Nh]^T) for a [M,K] and w_pair [2 Nh, K] (the stacked
+    folded BilinearIntermediate weights) as ONE split-K GEMM + one reduction that takes the product
+    (include/pipnet_amd.h pipnet_linear_pair_mul_f32)."""
+    require_device(a, "linear input")
+    _chk(w_pair, "paired weight")
+    m, k = a.shape
+    n2 = w_pair.shape[0]
+    if a.stride(1) != 1 or w_pair.shape[1] != k or n2 % 2:
+        raise RuntimeError(f"linear_pair_mul: shapes {tuple(a.shape)} x {tuple(w_pair.shape)}")
+    nh = n2 // 2
+    splits = max(1, splitk_factor(m, n2, k))
+    out = torch.empty((m, nh), device=a.device, dtype=torch.float32)
+    ws = torch.empty((splits, m, n2), device=a.device, dtype=torch.float32)
+    _launch("pipnet_gemm::gemm_f32_tn_kernel<32, 1, 0, 0, 3, 2, 0, false>", 2.0 * m * n2 * k,
+            lambda: _lib.call("pipnet_linear_pair_mul_f32", a.data_ptr(), a.stride(0), w_pair.data_ptr(),
+                              out.data_ptr(), out.stride(0), m, nh, k, splits, ws.data_ptr(), _stream(a)))
+    return out
+
+
 def matmul_f64acc(a: Tensor, b: Tensor) -> Tensor:
     """[M,K] @ [K,N] (row-major fp32) with fp64 products and sums, rounded once to fp32
     (include/pipnet_amd.h pipnet_matmul_f64acc_f32): the inference-time weight folds."""
@@ -665,8 +685,8 @@ def softmax_pool_linear(feat_nhwc: Tensor, w: Tensor, bias: Optional[Tensor], th
     return proto, pooled, x_out, logits
 
 
-# Fused-head scratch, one (partials, tickets) pair per (device, stream): the tickets are zeroed once
-# here, in a buffer of their own, and left zero by every completed launch (include/pipnet_amd.h), so
+# Fused-head scratch, one (running maxima, tickets) pair per (device, stream): both are zeroed once
+# here and left zero by every completed launch (include/pipnet_amd.h), so
 # the head needs no memset per call; per stream because two concurrent heads (the split forward's
 # sub-batch streams) must not share them.  Buffers only grow; a grown one is allocated (zeroed) on
 # the stream that uses it.
@@ -678,7 +698,7 @@ def _head_workspace(dev: torch.device, stream: int, nfloats: int, b: int) -> Tup
     part, tickets = _HEAD_WS.get(key, (None, None))
     capturing = torch.cuda.is_current_stream_capturing()
     if part is None or part.numel() < nfloats:
-        part = torch.empty(max(nfloats, 4), device=dev, dtype=torch.float32)
+        part = torch.zeros(max(nfloats, 4), device=dev, dtype=torch.float32)
     if tickets is None or tickets.numel() < b:
         tickets = torch.zeros(max(b, 64), device=dev, dtype=torch.int32)
     if not capturing:          # graph-owned buffers (their zero-fill replays with them) are never cached

@@ -28,6 +28,11 @@ from .resnet_features import (resnet18_features, resnet34_features, resnet50_fea
                               resnet101_features, resnet152_features)
 
 PRESENCE_THRESHOLD = 0.1   # pipnet.py:36
+# The head as ONE launch (softmax_pool_linear: the classifier GEMV in each image's last workgroup)
+# or as softmax_pool + nonneg_linear; bitwise equal.  The two-kernel form is the default: the
+# one-launch form runs each image's 200-class GEMV serially in one workgroup at the end of the
+# pooling kernel and measured C2 -0.5 %, C3 -3.9 % (profiles/r05/ab_fused_head.txt).
+FUSED_HEAD = False
 
 
 class PIPNet(nn.Module):
@@ -72,13 +77,16 @@ class PIPNet(nn.Module):
         return add_on_logits_hip(self._add_on, feats)      # [B,h,w,P]
 
     def _hip_head(self, logits: Tensor, inference: bool, out=None):
-        """softmax + max-pool + threshold + NonNegLinear as ONE kernel launch (the classifier runs
-        in the last workgroup of each image, include/pipnet_amd.h pipnet_softmax_pool_linear_f32);
-        ``out`` = (proto, pooled, clamped, logits) tensors to write into (batch slices of the
-        split forward)."""
+        """softmax + max-pool (pipnet_softmax_pool_*), then threshold + NonNegLinear
+        (pipnet_nonneg_linear_f32) -- or the same as one launch (FUSED_HEAD); ``out`` = (proto,
+        pooled, clamped, logits) tensors to write into (batch slices of the split forward)."""
         cls = self._classification
-        proto, pooled, clamped, res = K.softmax_pool_linear(
-            logits, cls.weight, cls.bias, PRESENCE_THRESHOLD if inference else None, out=out)
+        thresh = PRESENCE_THRESHOLD if inference else None
+        if FUSED_HEAD:
+            return K.softmax_pool_linear(logits, cls.weight, cls.bias, thresh, out=out)
+        pool = K.softmax_pool_bf16 if logits.dtype == torch.bfloat16 else K.softmax_pool
+        proto, pooled = pool(logits, 0, out=None if out is None else out[:2])
+        clamped, res = K.nonneg_linear(pooled, cls.weight, cls.bias, thresh, out=None if out is None else out[2:])
         return proto, pooled, clamped, res
 
     def _forward_hip_split(self, xs: Tensor, inference: bool, n: int):

@@ -87,6 +87,12 @@ int pipnet_linear_splitk_f32(const float* A, int64_t lda, const float* W, const 
                              const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,
                              int M, int N, int K, int epilogue, int splits, float* workspace,
                              void* stream);
+/* BilinearIntermediate on the folded pair in one GEMM: Wpair = [W1; W2] ([2 Nh, K], the
+ * pipnet_matmul2_f64acc_f32 output), C[M, Nh] = (A W2^T) * (A W1^T) elementwise, K split into
+ * `splits` slabs (workspace: splits * M * 2 Nh floats) summed in slab order by the reduction that
+ * also takes the product -- count_pipnet_utils.py:378-385 W(e) * V(e) with e folded in. */
+int pipnet_linear_pair_mul_f32(const float* A, int64_t lda, const float* Wpair, float* C, int64_t ldc, int M, int Nh,
+                               int K, int splits, float* workspace, void* stream);
 
 /* ConvNeXt downsample conv, k=2, stride s in {1,2}, no padding, as implicit GEMM on MFMA.
  * x: [B,H,W,Cin] NHWC (already LayerNorm2d-normalised), w_packed: [Cout][2][2][Cin]
@@ -228,11 +234,11 @@ int pipnet_softmax_pool_bf16(const void* feat, int B, int HW, int P, int pool_mo
  * written to x_out [B,P] (may be NULL), and out [B,K] = x' relu(W)^T + bias, W [K,P] read at
  * call time.  Bitwise equal to the two-kernel path.  W 16-B aligned when P % 4 == 0.  _bf16:
  * bf16 logits.
- * part: pipnet_softmax_pool_linear_part_floats(B, HW, P) floats of scratch (per-pixel-block
- * maxima).  tickets: int32 [B] arrival counters that must be ZERO on entry -- zero them once at
- * allocation: every completed call leaves tickets[0..B) zero again, so no memset is needed
- * between calls.  Keep them in their own buffer (never let other data overwrite them) and give
- * calls that may run concurrently (different streams) separate part / tickets buffers. */
+ * part: pipnet_softmax_pool_linear_part_floats(B, HW, P) (= B * P) floats of scratch for the
+ * running maxima, tickets: int32 [B] arrival counters -- BOTH must be ZERO on entry: zero them once
+ * at allocation; every completed call leaves part[0 .. B*P) and tickets[0 .. B) zero again, so no
+ * memset is needed between calls.  Calls that may run concurrently (different streams) need
+ * separate part / tickets buffers. */
 int64_t pipnet_softmax_pool_linear_part_floats(int B, int HW, int P);
 int pipnet_softmax_pool_linear_f32(const float* feat, int B, int HW, int P, float* proto, float* pooled,
                                    const float* W, const float* bias, int K, int apply_thresh, float thresh,

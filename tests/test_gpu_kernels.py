@@ -430,8 +430,8 @@ def test_fused_head_bitwise_two_kernel_path(gpu, dtype, b, hw, p, k, thresh):
     proto3, pooled3, xo3, out3 = K.softmax_pool_linear(f4, w, bias, thresh, out=(proto, pooled, xo, out.clone()))
     torch.cuda.synchronize()
     assert torch.equal(out3, out2) and torch.equal(pooled3, pooled2)
-    _, tickets = K._HEAD_WS[(f4.device.index, torch.cuda.current_stream(f4.device).cuda_stream)]
-    assert int(tickets.abs().sum().item()) == 0        # tickets reset by the launch
+    pmax, tickets = K._HEAD_WS[(f4.device.index, torch.cuda.current_stream(f4.device).cuda_stream)]
+    assert int(tickets.abs().sum().item()) == 0 and float(pmax.abs().sum().item()) == 0.0   # reset by the launch
 
 
 def test_fused_head_is_one_launch(gpu):

@@ -4,6 +4,7 @@
     python tools/ab_toggle.py <module>.<FLAG> <config> [--rounds 5] [--steps 10]
 e.g. count_pipnet_amd.resnet_hip.DUAL_1X1 c3  (arms False, True)
 Stream splits as arms: streams:1:2:3.
+An int module attribute per arm: attr:<module>.<NAME>:<v>:<v>[...].
 A library switch function instead of a module flag: fn:<module>.<func>:<arg>:<arg>[:<arg>...],
 one arm per argument, e.g. fn:module.setter:0:1 (a setter function called with each value).  Prints one JSON line per arm and whether
 every arm's outputs are bitwise equal to the first arm's."""
@@ -44,6 +45,14 @@ def main():
 
         def switch(val):
             fn(val)
+    elif a.flag.startswith("attr:"):           # attr:<module>.<NAME>:<v>:<v>... -- an int module attribute per arm
+        parts = a.flag.split(":")
+        modname, attr = parts[1].rsplit(".", 1)
+        mod = importlib.import_module(modname)
+        arms = [int(v) for v in parts[2:]]
+
+        def switch(val):
+            setattr(mod, attr, val)
     else:
         modname, attr = a.flag.rsplit(".", 1)
         mod = importlib.import_module(modname)
