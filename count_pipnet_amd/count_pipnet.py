@@ -203,13 +203,22 @@ def intermediate_hip(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
     if isinstance(layer, LinearFull):
         return K.linear(x, layer.linear.weight)
     if isinstance(layer, BilinearIntermediate):
-        wf, vf = _bilinear_folded(layer)
+        wf, vf, pair = _bilinear_folded(layer)
+        if BILINEAR_PAIR and x.shape[1] % 32 == 0 and wf.shape[0] % 4 == 0 and x.stride(0) % 4 == 0:
+            return K.linear_pair_mul(x, pair)     # one split-K GEMM over [W E; V E] + one product reduction
         we = K.linear(x, wf)
         return K.linear(x, vf, epilogue=_lib.EPI_MUL, r=we)
     raise RuntimeError(f"CountPIPNet HIP path: unsupported intermediate layer {type(layer).__name__}")
 
 
-def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.Tensor]:
+# BilinearIntermediate at inference: both folded products as ONE split-K GEMM over the stacked
+# [W E; V E] weights whose reduction multiplies the two halves (K.linear_pair_mul; needs P % 32 == 0
+# and D % 4 == 0), else as two GEMMs with the product in the second's epilogue (also the A/B arm;
+# the same products, slab sums may group differently).
+BILINEAR_PAIR = True
+
+
+def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """W(embed(x)) * V(embed(x)) (count_pipnet_utils.py:378-385) with the embedding folded into
     both projections: the three Linears carry no bias and nothing sits between embed and W / V,
     so W(E x) = (W E) x.  The folded [D, P] weights (W E, V E; products taken in fp64, rounded
@@ -229,8 +238,8 @@ def _bilinear_folded(layer: BilinearIntermediate) -> Tuple[torch.Tensor, torch.T
     if ent is None or ent[0] != stamp:
         with torch.no_grad():
             e = layer.embed.weight.detach().contiguous()
-            wf, vf = K.matmul2_f64acc(layer.W.weight.detach().contiguous(), layer.V.weight.detach().contiguous(), e)
-        ent = (stamp, (wf, vf))
+            pair = K.matmul2_f64acc(layer.W.weight.detach().contiguous(), layer.V.weight.detach().contiguous(), e)
+        ent = (stamp, (pair[0], pair[1], pair.view(-1, pair.shape[2])))    # [W E; V E] stacked: [2 D, P]
         cache[key] = ent
         packed_ready()
     return ent[1]

@@ -162,9 +162,9 @@ def matmul_f64acc(a: Tensor, b: Tensor) -> Tensor:
     return out
 
 
-def matmul2_f64acc(a0: Tensor, a1: Tensor, b: Tensor) -> Tuple[Tensor, Tensor]:
-    """(a0 @ b, a1 @ b) as ``matmul_f64acc`` in ONE launch (pipnet_matmul2_f64acc_f32): the
-    bilinear fold's W.E and V.E share the embedding operand."""
+def matmul2_f64acc(a0: Tensor, a1: Tensor, b: Tensor) -> Tensor:
+    """torch.stack((a0 @ b, a1 @ b)) ([2, M, N]) as ``matmul_f64acc`` in ONE launch
+    (pipnet_matmul2_f64acc_f32): the bilinear fold's W.E and V.E share the embedding operand."""
     for t, what in ((a0, "fold operand A0"), (a1, "fold operand A1"), (b, "fold operand B")):
         _chk(t, what)
     if a0.dim() != 2 or a0.shape != a1.shape or b.dim() != 2 or a0.shape[1] != b.shape[0]:
@@ -174,7 +174,7 @@ def matmul2_f64acc(a0: Tensor, a1: Tensor, b: Tensor) -> Tuple[Tensor, Tensor]:
     out = torch.empty((2, m, n), device=a0.device, dtype=torch.float32)
     _lib.call("pipnet_matmul2_f64acc_f32", a0.data_ptr(), a1.data_ptr(), k, b.data_ptr(), n, out[0].data_ptr(),
               out[1].data_ptr(), n, m, n, k, _stream(a0))
-    return out[0], out[1]
+    return out
 
 
 def linear_rowscale(a: Tensor, w: Tensor, bias: Optional[Tensor], scale: Tensor, r: Tensor, row_scale: Tensor,

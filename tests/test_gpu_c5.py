@@ -142,6 +142,28 @@ def test_matmul2_f64acc_pair_equals_singles(gpu):
         assert torch.equal(c0, K.matmul_f64acc(a0, b)) and torch.equal(c1, K.matmul_f64acc(a1, b)), (m, n, k)
 
 
+def test_linear_pair_mul_equals_two_gemms(gpu):
+    """pipnet_linear_pair_mul_f32 (one split-K GEMM over the stacked [W E; V E] + a reduction
+    taking the product) = the two-GEMM form (V E x) * (W E x) bitwise when both split K into the
+    same slabs, and the fp64 product at 1e-5 relative, on the C5 shape, short M, ragged M and long M
+    (no split)."""
+    from count_pipnet_amd import _lib
+    from count_pipnet_amd import kernels as K
+    g = torch.Generator().manual_seed(13)
+    for m, nh, k in [(64, 2048, 6144), (3, 2048, 6144), (37, 256, 512), (1000, 128, 256)]:
+        x = torch.randint(0, 4, (m, k), generator=g).float()
+        w = torch.randn(2 * nh, k, generator=g) / k ** 0.5
+        out = K.linear_pair_mul(x.to(gpu), w.to(gpu)).cpu()
+        wd, xd = w.double(), x.double()
+        ref = (xd @ wd[nh:].t()) * (xd @ wd[:nh].t())
+        scale = ref.abs().max().clamp(min=1.0)
+        assert ((out.double() - ref).abs() / scale).max().item() <= 1e-5, (m, nh, k)
+        if 1 < K.splitk_factor(m, 2 * nh, k) == K.splitk_factor(m, nh, k):
+            we = K.linear(x.to(gpu), w[:nh].contiguous().to(gpu))
+            two = K.linear(x.to(gpu), w[nh:].contiguous().to(gpu), epilogue=_lib.EPI_MUL, r=we).cpu()
+            assert torch.equal(out, two), (m, nh, k)
+
+
 def test_bilinear_fold_tracks_weight_updates(gpu):
     """The folded (W E, V E) weights follow every in-place update that bumps a parameter's
     version (optimizer-style ``copy_``/``add_``, ``load_state_dict``); a ``.data`` write is
