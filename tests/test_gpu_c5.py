@@ -150,7 +150,7 @@ def test_linear_pair_mul_equals_two_gemms(gpu):
     from count_pipnet_amd import _lib
     from count_pipnet_amd import kernels as K
     g = torch.Generator().manual_seed(13)
-    for m, nh, k in [(64, 2048, 6144), (3, 2048, 6144), (37, 256, 512), (1000, 128, 256)]:
+    for m, nh, k in [(64, 6144, 2048), (3, 6144, 2048), (37, 256, 512), (1000, 128, 256)]:
         x = torch.randint(0, 4, (m, k), generator=g).float()
         w = torch.randn(2 * nh, k, generator=g) / k ** 0.5
         out = K.linear_pair_mul(x.to(gpu), w.to(gpu)).cpu()
