@@ -10,8 +10,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BENCH = os.path.join(REPO, "profiles", "r04", "bench_final.json")
-STATS = os.path.join(REPO, "profiles", "r04", "kernel_stats_bench_final.csv")
+BENCH = os.path.join(REPO, "profiles", "r05", "bench_final.json")
+STATS = os.path.join(REPO, "profiles", "r05", "kernel_stats_bench_final.csv")
 
 
 @pytest.mark.skipif(not (os.path.exists(BENCH) and os.path.exists(STATS)), reason="no kept evidence")
