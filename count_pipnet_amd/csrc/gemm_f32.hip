@@ -34,6 +34,10 @@ int gemm_variant(int M, int N, int K, bool vec) {
   if (K % 32) return K % 16 == 0 && M > 64 ? 1 : 0;
   if (PIPNET_AB_GEMM_RULE == 1 && N == 384 && K >= 1536 && M > 64) return 3;   // stage-3 fc2 on 128-row tiles
   if (PIPNET_AB_GEMM_RULE == 2 && N == 1536 && K == 384) return 2;              // stage-3 fc1 on 64-row tiles
+  // wide short-K (C5's add-on 1x1 conv, 192 -> 2048 prototypes): 128-row tiles -- 2,048 tiles in
+  // four full rounds of 2 per CU instead of 4,096 64-row tiles in 5.3 rounds of 3; C5 +0.8 % in
+  // four interleaved rounds (profiles/r05/ab_c5_addon_tile.txt).  Same K order: bitwise equal.
+  if (N >= 1024 && N % BN == 0 && K <= 192 && M > 64) return 3;
   if (N <= 384 || K <= 192 || M <= 64) return 2;
   return 3;
 }

@@ -42,6 +42,8 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
         return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if k % 32:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
+    if n >= 1024 and n % 128 == 0 and k <= 192 and m > 64:
+        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
     if n <= 384 or k <= 192 or m <= 64:
         npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
