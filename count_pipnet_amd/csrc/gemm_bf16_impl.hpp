@@ -1474,7 +1474,7 @@ namespace spool {
 constexpr int NT = 384, PR = 2, SR = 2 * PR + 1, IR = SR + 3, N = 64, K = 256;
 constexpr int MAX_OW = 112, BLOCKS = 18;              // 18 x 32 >= SR x MAX_OW = 560 stem pixels
 constexpr int IN_BYTES = 30 * 1024, OFF_WT = IN_BYTES, WT_BYTES = N * K * 2;
-constexpr int OUT_BYTES = SR * MAX_OW * N * 2;        // 70 KiB of bf16 stem rows
+constexpr int OUT_BYTES = BLOCKS * 32 * N * 2;        // 72 KiB of bf16 stem rows (576 >= SR x MAX_OW: padding rows too)
 constexpr int SMEM = OUT_BYTES > OFF_WT + WT_BYTES ? OUT_BYTES : OFF_WT + WT_BYTES;
 static_assert(2 * SMEM <= 160 * 1024, "two workgroups per CU");
 static_assert(BLOCKS * 32 >= SR * MAX_OW && BLOCKS == 3 * (NT / 64), "3 blocks per wave");
@@ -1551,7 +1551,9 @@ __global__ __launch_bounds__(spool::NT, 2) void stem_pool_bf16_kernel(const bf16
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // staging area free
 
-  // ---- stem rows to LDS as bf16: relu(acc + b), rounded as tile 6's epilogue rounds ----
+  // ---- stem rows to LDS as bf16: relu(acc + b), rounded as tile 6's epilogue rounds.  Every
+  // block's 32 rows are written, padding rows past SR x OW included (the buffer holds all 576):
+  // no per-element guard (a guarded store per element made hipcc branch and wait around each) ----
   bf16* out = reinterpret_cast<bf16*>(smem);
   const float bj[2] = {bias[lr], bias[32 + lr]};
 #pragma unroll
@@ -1561,32 +1563,43 @@ __global__ __launch_bounds__(spool::NT, 2) void stem_pool_bf16_kernel(const bf16
 #pragma unroll
       for (int v = 0; v < 16; ++v) {
         const int m = 32 * (3 * wid + i) + (v & 3) + 8 * (v >> 2) + 4 * lh;
-        if (m < SR * OW) out[m * N + 32 * j + lr] = (bf16)fmaxf(acc[i][j][v] + bj[j], 0.f);
+        out[m * N + 32 * j + lr] = (bf16)fmaxf(acc[i][j][v] + bj[j], 0.f);
       }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
-  // ---- MaxPool2d(3, 2, 1) over the stem rows, 8 channels per item ----
-  for (int it = tid; it < PR * PW * 8; it += NT) {
-    const int c8 = it & 7, px = (it >> 3) % PW, py = PR * pr + (it >> 3) / PW;
-    if (py >= PH) continue;
-    float mx[8];
+  // ---- MaxPool2d(3, 2, 1) over the stem rows, 8 channels per item: lane group (tid >> 3) walks
+  // the pooled columns, no division.  Window taps outside the stem map are clamped onto an edge
+  // tap of the same window (max is idempotent, so the duplicate changes nothing) instead of being
+  // skipped: the nine reads carry no branch.  Same fmaxf chain from -inf in (ky, kx) order over
+  // the in-range taps, with duplicates inserted -- bitwise the unfused pool's result ----
+  const int c8 = tid & 7;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
-    for (int ky = 0; ky < 3; ++ky) {
-      const int oy = 2 * py - 1 + ky;
-      if (oy < 0 || oy >= OH) continue;
-      for (int kx = 0; kx < 3; ++kx) {
-        const int ox = 2 * px - 1 + kx;
-        if (ox < 0 || ox >= OW) continue;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(out + ((oy - oy0) * OW + ox) * N + 8 * c8);
+  for (int r = 0; r < PR; ++r) {
+    const int py = PR * pr + r;
+    if (py >= PH) break;
+    int lrow[3];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
-      }
+    for (int ky = 0; ky < 3; ++ky) lrow[ky] = min(max(2 * py - 1 + ky, 0), OH - 1) - oy0;
+    for (int px = tid >> 3; px < PW; px += NT / 8) {
+      int col[3];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) col[kx] = min(max(2 * px - 1 + kx, 0), OW - 1);
+      float mx[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) mx[e] = -INFINITY;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(out + (lrow[ky] * OW + col[kx]) * N + 8 * c8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx[e] = fmaxf(mx[e], (float)v[e]);
+        }
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (bf16)mx[e];
+      *reinterpret_cast<bf16x8*>(Y + (((int64_t)b * PH + py) * PW + px) * N + 8 * c8) = o;
     }
-    bf16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (bf16)mx[e];
-    *reinterpret_cast<bf16x8*>(Y + (((int64_t)b * PH + py) * PW + px) * N + 8 * c8) = o;
   }
 }
 
