@@ -64,7 +64,10 @@ struct MlpGeo {
 // Launch bounds: at least 2 waves per SIMD for every workgroup size (MINB = 8 / NW workgroups per
 // CU), so the register allocation stays within 256 -- with the plain 256-thread bound hipcc spread
 // the C = 192 kernels over 198 VGPRs + 70 AGPRs, one wave per SIMD.
-template <int C, int HC, int NW, int PX, int HS = 1>
+// ABL (tuning lab only, tools/mlp_lab.hip; 0 in the product): 1 = no GELU, 2 = no per-chunk
+// barrier / DMA wait, 4 = no GEMM2 (h added into acc), 8 = no GEMM1, 16 = no weight DMA
+// (profiles/r05/mlp_ablation.txt).
+template <int C, int HC, int NW, int PX, int HS = 1, int ABL = 0>
 __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_kernel(const float* __restrict__ t, const float* __restrict__ W1,
                                                               const float* __restrict__ b1,
                                                               const float* __restrict__ W2,
@@ -107,6 +110,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_ker
     }
   }
   auto stage = [&](int ch) {                           // ch = chunk index within a part
+    if constexpr ((ABL & 16) != 0) return;
     float* base = smem + (ch % NSTG) * G::STAGE_F;
 #pragma unroll
     for (int j = 0; j < G::PPW; ++j) {
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_ker
 
   for (int ci = 0; ci < G::NCHH; ++ci) {
     // this wave's pieces of stage ci landed, every wave's reads of stage ci-1 retired
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if constexpr ((ABL & 2) == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (ci + 1 < G::NCHH) stage(ci + 1);                // into the buffer of stage ci-1
     const float* buf = smem + (ci & 1) * G::STAGE_F + part * G::CHUNK_F;
     const int ch = part * G::NCHH + ci;                 // global hidden chunk
@@ -157,6 +161,12 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_ker
     for (int u = 0; u < PX; ++u)
 #pragma unroll
       for (int hb = 0; hb < NHB; ++hb) h[u][hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr ((ABL & 8) != 0) {
+#pragma unroll
+      for (int u = 0; u < PX; ++u)
+#pragma unroll
+        for (int hb = 0; hb < NHB; ++hb) h[u][hb] = tb[u][hb % (C / 16)] + ld4(buf + w1_off(hb, 0));
+    } else
 #pragma unroll
     for (int g = 0; g < C / 16; ++g) {
       f32x4 w[NHB];
@@ -177,12 +187,22 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_ker
 #pragma unroll
       for (int u = 0; u < PX; ++u) {
         const f32x4 v = h[u][hb] + bb;
+        if constexpr ((ABL & 1) != 0) {
+          h[u][hb] = v;
+          continue;
+        }
         const f32x2 lo = gelu_pk16(f32x2{v[0], v[1]}), hi = gelu_pk16(f32x2{v[2], v[3]});
         h[u][hb] = f32x4{lo[0], lo[1], hi[0], hi[1]};
       }
     }
     // GEMM2: out^T[c][pixel] += W2[c][hidden] h^T[hidden][pixel]; the cb loop innermost, so
     // consecutive MFMAs go to different accumulators
+    if constexpr ((ABL & 4) != 0) {
+#pragma unroll
+      for (int u = 0; u < PX; ++u)
+#pragma unroll
+        for (int hb = 0; hb < NHB; ++hb) acc[u][hb % (C / 16)] += h[u][hb] * ld4(buf + w2_off(hb % (C / 16), hb));
+    } else
 #pragma unroll
     for (int hb = 0; hb < NHB; ++hb) {
       f32x4 w[C / 16];
@@ -244,11 +264,11 @@ __global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_ker
   }
 }
 
-template <int C, int HC, int NW, int PX, int HS = 1>
+template <int C, int HC, int NW, int PX, int HS = 1, int ABL = 0>
 int launch_mlp(const float* t, const float* W1, const float* b1, const float* W2, const float* b2, const float* gamma,
                float* x, int M, hipStream_t s) {
   const int px = 16 * PX * NW / HS;
-  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX, HS>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1,
+  hipLaunchKernelGGL((cnblock_mlp_kernel<C, HC, NW, PX, HS, ABL>), dim3((M + px - 1) / px), dim3(64 * NW), 0, s, t, W1,
                      b1, W2, b2, gamma, x, M);
   PIPNET_CHECK_LAUNCH();
   return PIPNET_OK;
