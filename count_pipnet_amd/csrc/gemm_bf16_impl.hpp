@@ -1082,7 +1082,10 @@ struct Lay {
 // RB = 16-row blocks per wave group: 8 -> 256-row tiles, 7 -> 224-row tiles (fewer idle CUs in
 // the last round of tiles, conv_bf16.hip pick_rb).  Every output element is the same MFMA chain
 // over the same K order whatever RB is, so the choice never changes a bit of the result.
-template <int EPI, int NB = 4, int RB = 8>
+// ABL (tuning lab only, tools/bf16_lab.hip lab_halo; 0 in the product): 1 = no B DMA, 2 = no
+// epilogue (one store per lane keeps the accumulators live), 4 = no barriers, 8 = no A fragment
+// reads after the first, 16 = no halo DMA after pair 0 (stale LDS / registers: timing only).
+template <int EPI, int NB = 4, int RB = 8, int ABL = 0>
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
   using namespace pp;
   using ph::NS;
@@ -1154,6 +1157,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   if (tid < 16) *reinterpret_cast<u32x4*>(smem + L::OFF_ZERO + 16 * tid) = u32x4{0u, 0u, 0u, 0u};
 
   auto stage_b = [&](int kt) {
+    if constexpr ((ABL & 1) != 0) {
+      if (kt > 1) return;
+    }
     const int P = kt / 18, rem = kt - 18 * P;
     const int k0 = (rem >> 1) * p.Cin + (2 * P + (rem & 1)) * BK;
     unsigned char* base = smem + (kt % NS) * L::BSTAGE;
@@ -1163,6 +1169,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
                                        (__attribute__((address_space(3))) void*)(base + bdst[i]), 16, 0, 0);
   };
   auto stage_halo = [&](int P) {
+    if constexpr ((ABL & 16) != 0) {
+      if (P > 0) return;
+    }
     unsigned char* base = smem + L::OFF_HALO + (P & 1) * 2 * L::HALO_BYTES;
 #pragma unroll
     for (int i = 0; i < L::HPW; ++i)
@@ -1178,7 +1187,12 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   };
   const unsigned char* zb = smem + L::OFF_ZERO;
   // lane byte offset inside a halo slot for this tap (fragment rows j add j * 1 KiB)
+  bool a_once = false;
   auto read_a = [&](bf16x8v (&fa)[4], const unsigned char* hb, int half, int loff, unsigned tbit) {
+    if constexpr ((ABL & 8) != 0) {
+      if (a_once) return;
+      if (half) a_once = true;
+    }
     const unsigned char* zl = zb + (loff & 255);
 #pragma unroll
     for (int r = 0; r < (half ? RB - 4 : 4); ++r) {
@@ -1209,6 +1223,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   // are B(kt+2) and the halo pieces issued at (0, 1) or, for (1, 0), one K-tile earlier; none
   // in the last tap of the last pair.  Everything but the MFMA stream is scalar bookkeeping
   // kept branch-light (one compile-time h per unrolled half).
+  auto hbar = [&]() {
+    if constexpr ((ABL & 4) == 0) pp_barrier();
+  };
   bf16x8v fa[4], fb[NB];
   const int lrow = wr * 16 * RB + fr;
   int kt = 0;
@@ -1229,7 +1246,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
         if (!last) stage_b(kt + 2);
         read_b(fb, st);
         read_a(fa, hb, 0, loff, tbit);
-        pp_barrier();
+        hbar();
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -1237,14 +1254,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
           for (int n = 0; n < NB; ++n)
             acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        pp_barrier();
+        hbar();
         // ---- phase 1: rows 64..127 ----
         if (h == 1 && t == 0 && more) stage_halo(P + 1);
         read_a(fa, hb, 1, loff, tbit);
         if (last) pp_wait_vm<0>();
         else if (more && ((h == 1 && t == 0) || (h == 0 && t == 1))) pp_wait_vm<L::BPW + L::HPW>();
         else pp_wait_vm<L::BPW>();
-        pp_barrier();
+        hbar();
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int r = 0; r < RB - 4; ++r)
@@ -1252,13 +1269,24 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
           for (int n = 0; n < NB; ++n)
             acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        pp_barrier();
+        hbar();
       }
     }
   }
-  if (wr == 0) pp_barrier();                                   // re-align the groups
+  if (wr == 0) hbar();                                   // re-align the groups
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pp_barrier();                                                // stage / halo buffers free for the epilogue
+  if constexpr ((ABL & 2) != 0) {
+    float tsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) tsum += acc[r][n][e];
+    reinterpret_cast<float*>(p.C)[(int64_t)blockIdx.x * pp::NT + tid] = tsum;
+    return;
+  }
   pp_epilogue<EPI, NB, RB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
 }
 

@@ -724,6 +724,37 @@ int group_for(int K, double budget) {
 }
 }  // namespace
 
+// 3x3 / stride 1 / pad 1 conv on the LDS-halo ping-pong tile (conv3x3_bf16_halo_kernel, product tile 8)
+// with its ABL ablation bits (0 = the product kernel, EPI_NONE): x NHWC [B][H][W][Cin] bf16, w packed
+// [N][9 Cin] bf16, y NHWC [B][H][W][N] bf16.  Same ConvParams as pipnet_conv2d_nhwc_bf16_tile.
+extern "C" int lab_halo(int abl, const void* x, int B, int H, int W, int Cin, const void* w, int N, void* y,
+                        void* stream) {
+  ConvParams p{};
+  p.A = reinterpret_cast<const bf16*>(x);
+  p.W = reinterpret_cast<const bf16*>(w);
+  p.C = reinterpret_cast<bf16*>(y);
+  p.ldc = N;
+  p.M = B * H * W; p.N = N;
+  p.Kv = 9 * Cin;
+  p.K = (p.Kv + KPAD - 1) / KPAD * KPAD;
+  p.H = H; p.Wd = W; p.Cin = Cin; p.OH = H; p.OW = W; p.stride = 1; p.KW = 3; p.pad = 1; p.Cinp = Cin;
+  if (Cin % 64 || W > 31 || N % 256 || (int64_t)p.M * Cin >= ((int64_t)1 << 31)) return 1;
+  p.nt = N / 256;
+  p.mt = (p.M + 255) / 256;
+  p.group_m = group_for(p.K, 2.0 * 1024 * 1024);
+  const dim3 grid(p.mt * p.nt);
+  hipStream_t s = (hipStream_t)stream;
+#define HALO_CASE(X) \
+  case X: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE, 4, 8, X>), grid, dim3(512), 0, s, p); break;
+  switch (abl) {
+    HALO_CASE(0) HALO_CASE(1) HALO_CASE(2) HALO_CASE(4) HALO_CASE(8) HALO_CASE(16) HALO_CASE(3) HALO_CASE(17)
+    HALO_CASE(19) HALO_CASE(10) HALO_CASE(12) HALO_CASE(27)
+    default: return 1;
+  }
+#undef HALO_CASE
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
 extern "C" int lab_pp(int abl, const void* A, const void* W, void* C, int M, int N, int K, double group_budget,
                       void* stream) {
   ConvParams p{};
