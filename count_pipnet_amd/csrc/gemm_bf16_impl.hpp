@@ -1085,8 +1085,9 @@ struct Lay {
 // ABL (tuning lab only, tools/bf16_lab.hip lab_halo; 0 in the product): 1 = no B DMA, 2 = no
 // epilogue (one store per lane keeps the accumulators live), 4 = no barriers, 8 = no A fragment
 // reads after the first, 16 = no halo DMA after pair 0 (stale LDS / registers: timing only).
-template <int EPI, int NB = 4, int RB = 8, int ABL = 0>
-__global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
+// (The body is a device function so that the product kernel's name carries no lab parameter.)
+template <int EPI, int NB, int RB, int ABL>
+__device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
   using namespace pp;
   using ph::NS;
   using L = ph::Lay<NB>;
@@ -1288,6 +1289,16 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
     return;
   }
   pp_epilogue<EPI, NB, RB>(p, acc, smem, m0, n0, wr, wc, lane, wid);
+}
+
+template <int EPI, int NB = 4, int RB = 8>
+__global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
+  conv3x3_bf16_halo_body<EPI, NB, RB, 0>(p);
+}
+
+template <int EPI, int NB, int RB, int ABL>   // tuning lab only (tools/bf16_lab.hip lab_halo)
+__global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_abl_kernel(ConvParams p) {
+  conv3x3_bf16_halo_body<EPI, NB, RB, ABL>(p);
 }
 
 // ======================================================================================

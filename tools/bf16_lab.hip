@@ -745,9 +745,10 @@ extern "C" int lab_halo(int abl, const void* x, int B, int H, int W, int Cin, co
   const dim3 grid(p.mt * p.nt);
   hipStream_t s = (hipStream_t)stream;
 #define HALO_CASE(X) \
-  case X: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE, 4, 8, X>), grid, dim3(512), 0, s, p); break;
+  case X: hipLaunchKernelGGL((conv3x3_bf16_halo_abl_kernel<PIPNET_EPI_NONE, 4, 8, X>), grid, dim3(512), 0, s, p); break;
   switch (abl) {
-    HALO_CASE(0) HALO_CASE(1) HALO_CASE(2) HALO_CASE(4) HALO_CASE(8) HALO_CASE(16) HALO_CASE(3) HALO_CASE(17)
+    case 0: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE, 4, 8>), grid, dim3(512), 0, s, p); break;
+    HALO_CASE(1) HALO_CASE(2) HALO_CASE(4) HALO_CASE(8) HALO_CASE(16) HALO_CASE(3) HALO_CASE(17)
     HALO_CASE(19) HALO_CASE(10) HALO_CASE(12) HALO_CASE(27)
     default: return 1;
   }
