@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "philox.hpp"
 
 namespace {
 // Zero-fill by a kernel rather than a memset call: the launch is captured as an ordinary
@@ -362,47 +363,8 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
   }
 }
 
-// ---------------------------------------------------------------------------------------
-// Philox4x32-10 (Salmon et al., SC'11) -> one Exp(1) draw per element index.
-// ---------------------------------------------------------------------------------------
-PIPNET_DEV uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t& hi) {
-  const uint64_t p = (uint64_t)a * b;
-  hi = (uint32_t)(p >> 32);
-  return (uint32_t)p;
-}
-
-// One Philox4x32-10 block: four 32-bit words for counter `ctr` under key `seed`.
-PIPNET_DEV void philox4(uint64_t seed, uint64_t ctr, uint32_t (&out)[4]) {
-  uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0u, c3 = 0u;
-  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    uint32_t hi0, hi1;
-    const uint32_t lo0 = mulhilo(0xD2511F53u, c0, hi0);
-    const uint32_t lo1 = mulhilo(0xCD9E8D57u, c2, hi1);
-    c0 = hi1 ^ c1 ^ k0;
-    c1 = lo1;
-    c2 = hi0 ^ c3 ^ k1;
-    c3 = lo0;
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  out[0] = c0, out[1] = c1, out[2] = c2, out[3] = c3;
-}
-
-PIPNET_DEV float exp1_from_bits(uint32_t w) {
-  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
-  return -logf(u);
-}
-
-// log E for E = -log u of the same 24-bit uniform, on the hardware log2 (v_log_f32, ~1 ulp):
-// ln E = ln2 * log2(-log2 u) + ln(ln2).  u in [2^-25, 1 - 2^-25] keeps both arguments normal.
-// For the hard Philox head only -- its noise is this library's own draw; the injected-noise and
-// soft paths keep the libm forms they share with the oracle.
-PIPNET_DEV float log_exp1_from_bits_fast(uint32_t w) {
-  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);
-  return fmaf(__builtin_amdgcn_logf(-__builtin_amdgcn_logf(u)), 0.69314718f, -0.36651292f);
-}
+// Philox4x32-10 and the Exp(1) / log Exp(1) draws: philox.hpp (shared with the fused add-on
+// GEMM's Gumbel epilogue, csrc/gemm_f32_impl.hpp).
 
 // One wave per pixel, four consecutive channels per lane (float4 logits / proto): the noise
 // of channels 4k..4k+3 of pixel (b, pix) is the Philox block (offset + (b*HW + pix)*P/4 + k)
@@ -550,7 +512,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void count_gumbel_kernel(const float*
         __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(proto + base + c));
       }
     }
-    if (lane == 0) atomicAdd(hist + (int64_t)b * P + mi, 1);
+    if (lane == 0 && (unsigned)mi < (unsigned)P) atomicAdd(hist + (int64_t)b * P + mi, 1);   // NaN rows: no argmax
   }
   if constexpr (SOFT) {
     __shared__ float red[HEAD_THREADS / 64][NJ4 * 256];

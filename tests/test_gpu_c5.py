@@ -196,3 +196,22 @@ def test_bilinear_fold_tracks_weight_updates(gpu):
         assert check() > 1e-3                                                 # stale, as documented
         assert invalidate_weight_caches(layer) >= 1
         assert check() < 1e-5
+
+
+# ---- the hard head's own Philox draw -------------------------------------------------------------
+
+def test_count_gumbel_philox_draws_are_finite(gpu):
+    """The Philox head on C5's full grid (64 x 256 pixels x 2,048 channels = 33.5M draws): every
+    one-hot value finite and within 1 ulp of 1.  Before round 5's clamp the hardware log2 returned
+    0 for uniforms within a few ulp of 1, giving log E = -inf, z = +inf and a NaN one-hot value
+    about twice per forward (csrc/philox.hpp log_exp1_from_bits_fast)."""
+    from count_pipnet_amd import kernels as K
+    g = torch.Generator().manual_seed(21)
+    logits = torch.randn(64, 16, 16, 2048, generator=g).to(gpu)
+    for seed in (987654321, 5, 2 ** 61 + 3):
+        proto, hist = K.count_gumbel(logits, 1.0, None, seed)
+        assert torch.isfinite(proto).all(), seed
+        nz = proto != 0
+        assert torch.equal(nz.sum(dim=-1), torch.ones_like(nz.sum(dim=-1)))
+        assert (proto[nz] - 1.0).abs().max().item() <= 2 ** -23
+        assert hist.sum().item() == 64 * 256
