@@ -22,8 +22,9 @@
 //     ds_read_b128 lane group of the fragment reads hits 16 distinct bank slots;
 //   * epilogue: lane l owns pixel l & 15 and 4 consecutive channels per tile -> one float4
 //     read-modify-write of x per tile, with gamma and b2.
-// k order of both contractions: t / hidden index 16 g + 4 q + s (q = lane >> 4, MFMA step s)
-// -- a different (equally exact) fp32 summation order than the unfused GEMMs.
+// k order of both contractions: t / hidden index 16 g + 4 q + s (q = lane >> 4, MFMA step s), GEMM1
+// as two chains over even / odd g summed at the end -- a different (equally exact) fp32 summation
+// order than the unfused GEMMs.
 #include "common.hpp"
 
 namespace {
@@ -66,7 +67,7 @@ struct MlpGeo {
 // the C = 192 kernels over 198 VGPRs + 70 AGPRs, one wave per SIMD.
 // ABL (tuning lab only, tools/mlp_lab.hip; 0 in the product): 1 = no GELU, 2 = no per-chunk
 // barrier / DMA wait, 4 = no GEMM2 (h added into acc), 8 = no GEMM1, 16 = no weight DMA
-// (profiles/r05/mlp_ablation.txt).
+// (profiles/r05/mlp_ablation.txt), 32 = GEMM1 on one accumulator chain (the round-2..4 form).
 // (The body is a device function so that the product kernel's name -- what rocprof reports and
 // bench.py / profiles/ key on -- carries no lab parameter; the lab launches cnblock_mlp_abl_kernel.)
 template <int C, int HC, int NW, int PX, int HS, int ABL>
@@ -148,6 +149,10 @@ __device__ __forceinline__ void cnblock_mlp_body(const float* __restrict__ t, co
     return G::W1F + r * HC + 4 * ((4 * hb + q) ^ G::f2(r));
   };
   constexpr int NHB = HC / 16;
+  // GEMM1 accumulator chains: 2 (even / odd t groups, summed after the chunk; lab bit 32 = the
+  // single chain of rounds 2-4): -0.6 / -1.8 / -2.3 / -0.2 % on C5 stage 1 / 2 and C2's stage 1 / 2
+  // half batches (profiles/r05/mlp_g1c.txt); a different -- equally exact -- fp32 association
+  constexpr int G1C = (ABL & 32) ? 1 : 2;
 
   for (int ci = 0; ci < G::NCHH; ++ci) {
     // this wave's pieces of stage ci landed, every wave's reads of stage ci-1 retired
@@ -167,19 +172,50 @@ __device__ __forceinline__ void cnblock_mlp_body(const float* __restrict__ t, co
       for (int u = 0; u < PX; ++u)
 #pragma unroll
         for (int hb = 0; hb < NHB; ++hb) h[u][hb] = tb[u][hb % (C / 16)] + ld4(buf + w1_off(hb, 0));
-    } else
+    } else if constexpr (G1C == 2) {
+      // two accumulator chains (even / odd t groups), added at the end: with one hidden block per
+      // chunk (HC = 16) a single chain issues each MFMA on the previous one's result
+      f32x4 h2[PX][NHB];
 #pragma unroll
-    for (int g = 0; g < C / 16; ++g) {
-      f32x4 w[NHB];
+      for (int u = 0; u < PX; ++u)
 #pragma unroll
-      for (int hb = 0; hb < NHB; ++hb) w[hb] = ld4(buf + w1_off(hb, g));
+        for (int hb = 0; hb < NHB; ++hb) h2[u][hb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+      for (int g = 0; g < C / 16; g += 2) {
+        f32x4 w[NHB], w2[NHB];
 #pragma unroll
-        for (int hb = 0; hb < NHB; ++hb)
+        for (int hb = 0; hb < NHB; ++hb) {
+          w[hb] = ld4(buf + w1_off(hb, g));
+          w2[hb] = ld4(buf + w1_off(hb, g + 1));
+        }
 #pragma unroll
-          for (int u = 0; u < PX; ++u)
-            h[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[hb][s], tb[u][g][s], h[u][hb], 0, 0, 0);
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int hb = 0; hb < NHB; ++hb)
+#pragma unroll
+            for (int u = 0; u < PX; ++u) {
+              h[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[hb][s], tb[u][g][s], h[u][hb], 0, 0, 0);
+              h2[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2[hb][s], tb[u][g + 1][s], h2[u][hb], 0, 0, 0);
+            }
+      }
+#pragma unroll
+      for (int u = 0; u < PX; ++u)
+#pragma unroll
+        for (int hb = 0; hb < NHB; ++hb) h[u][hb] = h[u][hb] + h2[u][hb];
+    } else {
+#pragma unroll
+      for (int g = 0; g < C / 16; ++g) {
+        f32x4 w[NHB];
+#pragma unroll
+        for (int hb = 0; hb < NHB; ++hb) w[hb] = ld4(buf + w1_off(hb, g));
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int hb = 0; hb < NHB; ++hb)
+#pragma unroll
+            for (int u = 0; u < PX; ++u)
+              h[u][hb] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[hb][s], tb[u][g][s], h[u][hb], 0, 0, 0);
+      }
     }
     // + b1, GELU (the unfused Linear1 epilogue's packed form)
 #pragma unroll

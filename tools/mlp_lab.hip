@@ -26,7 +26,7 @@ bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float*
   case 2000 + B: if (C != 192) return false; launch_mlp<192, 16, 8, 1, 1, B>(t, W1, b1, W2, b2, gamma, x, M, s); return true; \
   case 3000 + B: if (C != 96) return false; launch_mlp<96, 32, 8, 1, 1, B>(t, W1, b1, W2, b2, gamma, x, M, s); return true; \
   case 4000 + B: if (C != 192) return false; launch_mlp<192, 16, 8, 1, 2, B>(t, W1, b1, W2, b2, gamma, x, M, s); return true;
-    A(0) A(1) A(2) A(4) A(8) A(16) A(3) A(12) A(18)
+    A(0) A(1) A(2) A(4) A(8) A(16) A(3) A(12) A(18) A(32)
 #undef A
     default: return false;
   }
