@@ -352,6 +352,8 @@ def main():
         timer = GemmTimer()
         if instrument:
             kernels.set_launch_hook(timer)
+            if world > 1:
+                model.exchange_events = []      # the pooled + logits all-gather, event-timed per step
         torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
@@ -365,13 +367,24 @@ def main():
         elapsed = time.perf_counter() - t0
         timer.enabled = False
         kernels.set_launch_hook(None)
+        agg = timer.summary()
+        ev = getattr(model, "exchange_events", None)
+        if ev:
+            # the last `steps` exchanges are the timed ones; mean ms per step, max over ranks below
+            agg["__exchange_ms__"] = sum(e0.elapsed_time(e1) for e0, e1 in ev[-steps:]) / min(steps, len(ev))
+            model.exchange_events = None
         if world > 1:
-            t = torch.tensor([elapsed], device=dev)
+            t = torch.tensor([elapsed, agg.get("__exchange_ms__", 0.0)], device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-        return elapsed, timer.summary()
+            elapsed = float(t[0].item())
+            if "__exchange_ms__" in agg:
+                agg["__exchange_ms__"] = float(t[1].item())
+        return elapsed, agg
 
     def roofline(agg, steps, peak_of):
+        agg = {k: v for k, v in agg.items() if not k.startswith("__")}
+        # dominant kernel = largest total time per step (the one definition: tools/pmc_summary.py's
+        # `dominant:` line uses the same rule)
         dom = max(agg, key=lambda k: agg[k][2])
         n_l, fl, tt = agg[dom]
         peak = peak_of(dom)
@@ -399,9 +412,12 @@ def main():
         set_stream_split(inner, 1)
         el1, agg = timed(model, inp, batch, steps, max(1, a.warmup // 2), instrument=True, gw=gw)
         set_stream_split(inner, nsplit)
+        exch = agg.pop("__exchange_ms__", None)
         _, roof = roofline(agg, steps, peak_of)
         info = {"stream_split": nsplit, "roofline_pass": {"streams": 1, "instrumented": True,
                                                           "ms_per_step": el1 / steps * 1e3}}
+        if exch is not None:
+            info["exchange_ms_per_step"] = exch
         return el, roof, agg, info
 
     split = a.precision == "bf16x3"
@@ -430,8 +446,12 @@ def main():
                                f"BASELINE {cfg_name}" + (", split-bf16 GEMMs" if split else ""),
                    "num_classes": classes, "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                    "image_size": 224, "parallelism": f"dp{world}",
-                   "exchange": (("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
-                                + " all_gather(logits, pooled)") if world > 1 else None},
+                   "exchange": {"collective": ("rccl" if dist.get_backend() == "nccl" else dist.get_backend())
+                                + " all_gather_into_tensor([pooled | logits])", "collectives_per_step": 1,
+                                "ms_per_step": info.get("exchange_ms_per_step"),
+                                "timing": "HIP events around the packed all-gather on the current stream, "
+                                          "roofline pass, mean over the timed steps, max over ranks"}
+                               if world > 1 else None},
         "roofline": roof,
         "model_tflops": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3,
         "model_frac_of_f32_peak": GFLOP_C2 * a.batch / (ms * 1e-3) / 1e3 / PEAK_F32_TFLOPS,

@@ -204,7 +204,8 @@ def intermediate_hip(layer: nn.Module, x: torch.Tensor) -> torch.Tensor:
         return K.linear(x, layer.linear.weight)
     if isinstance(layer, BilinearIntermediate):
         wf, vf, pair = _bilinear_folded(layer)
-        if BILINEAR_PAIR and x.shape[1] % 32 == 0 and wf.shape[0] % 4 == 0 and x.stride(0) % 4 == 0:
+        if (BILINEAR_PAIR and x.shape[1] % 32 == 0 and wf.shape[0] % 4 == 0 and x.stride(0) % 4 == 0
+                and x.stride(1) == 1 and x.data_ptr() % 16 == 0):    # else the two-GEMM form
             return K.linear_pair_mul(x, pair)     # one split-K GEMM over [W E; V E] + one product reduction
         we = K.linear(x, wf)
         return K.linear(x, vf, epilogue=_lib.EPI_MUL, r=we)

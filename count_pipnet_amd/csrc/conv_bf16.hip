@@ -105,8 +105,11 @@ int halo_nb(int N) { return N >= 256 ? 4 : (N >= 128 ? 2 : 1); }
 // rounds: 6.00 vs 6.11 ms, profiles/r04/ab_c3_rb224.txt; the template keeps RB for the lab.)
 constexpr int PP_RB = 8;
 
+// The tile a launch takes (requested tile v >= 0 validated, v < 0 = the automatic choice), or -1
+// when the requested tile cannot run this conv.  The ONE tile rule: launch_conv dispatches on it
+// and pipnet_conv2d_nhwc_bf16_plan exports it, so profiling labels never mirror it in Python.
 template <int ALOAD>
-int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
+int plan_conv(const ConvParams& p, int epi, int v) {
   const bool pp_ok = (ALOAD == ALOAD_DENSE || p.Cin % 32 == 0) && p.K % 32 == 0;
   const bool hk = ALOAD == ALOAD_CONV && halo_ok(p, epi);
   const bool h64 = ALOAD == ALOAD_CONV && halo64_ok(p, epi);
@@ -118,7 +121,14 @@ int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
     else if (h64 && H64_AUTO) v = 11;
     else if (v == 5 && pk) v = 9;
   }
-  if (v > 11 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return PIPNET_ERR_ARG;
+  if (v > 11 || v == 10 || (v == 11 && !h64) || ((v == 5 || v == 7) && !pp_ok) || (v == 8 && !hk) || (v == 9 && !pk)) return -1;
+  return v;
+}
+
+template <int ALOAD>
+int launch_conv(ConvParams& p, int epi, int v, hipStream_t s) {
+  v = plan_conv<ALOAD>(p, epi, v);
+  if (v < 0) return PIPNET_ERR_ARG;
   if (v == 11) {                                 // Cin = N = 64 / 128 3x3 on the LDS input halo
     const int bm = p.N == 64 ? hsm::Shape<64>::BM : hsm::Shape<128>::BM;
     p.nt = 1;
@@ -357,32 +367,20 @@ __global__ __launch_bounds__(256) void maxpool_nhwc_bf16_kernel(const bf16* __re
   }
 }
 
-}  // namespace
-
-extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
-                                            const float* bias, int Cout, int KH, int KW, int stride, int pad,
-                                            const void* R, int epilogue, void* y, int tile, void* stream) {
+// Shape part of a bf16 conv's ConvParams (no pointers) -- shared by the launch and the plan query.
+// Returns PIPNET_OK or PIPNET_ERR_ARG; `dense` = the 1x1 stride-1 pad-0 plain-GEMM form.
+int conv_bf16_shape(ConvParams& p, bool& dense, int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                    int pad, int epilogue) {
   if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || (Cin & 7) || Cout <= 0 || (Cout & 7) || KH <= 0 || KW <= 0 ||
       stride <= 0 || pad < 0)
     return PIPNET_ERR_ARG;
   if (epilogue != PIPNET_EPI_NONE && epilogue != PIPNET_EPI_BIAS && epilogue != PIPNET_EPI_BIAS_RELU &&
       epilogue != PIPNET_EPI_BIAS_RESID_RELU)
     return PIPNET_ERR_ARG;
-  if (epilogue == PIPNET_EPI_BIAS_RESID_RELU && !R) return PIPNET_ERR_ARG;
-  if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
-  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y) || (R && !aligned16(R)) || (bias && !aligned16(bias)))
-    return PIPNET_ERR_ALIGN;
   const int OH = (H + 2 * pad - KH) / stride + 1, OW = (W + 2 * pad - KW) / stride + 1;
   if (OH <= 0 || OW <= 0) return PIPNET_ERR_ARG;
   if ((int64_t)B * OH * OW >= (int64_t)1 << 31) return PIPNET_ERR_ARG;
-  if (B == 0) return PIPNET_OK;
-  ConvParams p{};
-  p.A = reinterpret_cast<const bf16*>(x);
-  p.W = reinterpret_cast<const bf16*>(w_packed);
-  p.bias = bias;
-  p.R = reinterpret_cast<const bf16*>(R);
   p.ldr = Cout;
-  p.C = reinterpret_cast<bf16*>(y);
   p.ldc = Cout;
   p.M = B * OH * OW; p.N = Cout;
   p.Kv = KH * KW * Cin;
@@ -390,11 +388,40 @@ extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, 
   p.H = H; p.Wd = W; p.Cin = Cin; p.OH = OH; p.OW = OW; p.stride = stride; p.KW = KW; p.pad = pad;
   p.Cinp = Cin;
   p.seg = 0;
-  if (KH == 1 && KW == 1 && stride == 1 && pad == 0) {      // pointwise: plain GEMM over pixels
-    p.lda = Cin;
-    return launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream);
-  }
-  return launch_conv<ALOAD_CONV>(p, epilogue, tile, (hipStream_t)stream);
+  dense = KH == 1 && KW == 1 && stride == 1 && pad == 0;     // pointwise: plain GEMM over pixels
+  if (dense) p.lda = Cin;
+  return PIPNET_OK;
+}
+
+}  // namespace
+
+extern "C" int pipnet_conv2d_nhwc_bf16_tile(const void* x, int B, int H, int W, int Cin, const void* w_packed,
+                                            const float* bias, int Cout, int KH, int KW, int stride, int pad,
+                                            const void* R, int epilogue, void* y, int tile, void* stream) {
+  ConvParams p{};
+  bool dense = false;
+  if (const int st = conv_bf16_shape(p, dense, B, H, W, Cin, Cout, KH, KW, stride, pad, epilogue)) return st;
+  if (epilogue == PIPNET_EPI_BIAS_RESID_RELU && !R) return PIPNET_ERR_ARG;
+  if (!x || !w_packed || !y) return PIPNET_ERR_ARG;
+  if (!aligned16(x) || !aligned16(w_packed) || !aligned16(y) || (R && !aligned16(R)) || (bias && !aligned16(bias)))
+    return PIPNET_ERR_ALIGN;
+  if (B == 0) return PIPNET_OK;
+  p.A = reinterpret_cast<const bf16*>(x);
+  p.W = reinterpret_cast<const bf16*>(w_packed);
+  p.bias = bias;
+  p.R = reinterpret_cast<const bf16*>(R);
+  p.C = reinterpret_cast<bf16*>(y);
+  return dense ? launch_conv<ALOAD_DENSE>(p, epilogue, tile, (hipStream_t)stream)
+               : launch_conv<ALOAD_CONV>(p, epilogue, tile, (hipStream_t)stream);
+}
+
+extern "C" int pipnet_conv2d_nhwc_bf16_plan(int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                            int pad, int epilogue, int tile) {
+  ConvParams p{};
+  bool dense = false;
+  if (conv_bf16_shape(p, dense, B, H, W, Cin, Cout, KH, KW, stride, pad, epilogue)) return -PIPNET_ERR_ARG;
+  const int v = dense ? plan_conv<ALOAD_DENSE>(p, epilogue, tile) : plan_conv<ALOAD_CONV>(p, epilogue, tile);
+  return v < 0 ? -PIPNET_ERR_ARG : v;
 }
 
 extern "C" int pipnet_conv2d_nhwc_bf16(const void* x, int B, int H, int W, int Cin, const void* w_packed,

@@ -31,8 +31,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // * to_bf16x8: RNE to bf16 (v_cvt_pk_bf16_f32), then ReLU as v_pk_max_i16 against 0 on the packed
 //   pairs -- a bf16's bits order like an int16 (sign first), so max(bits, 0) zeroes exactly the
 //   negative values (-0 included) and keeps the rest: RNE(max(x, 0)) for every non-NaN x in one
-//   instruction per 2 elements instead of a v_max_f32 per element (a NaN now stays NaN, as torch's
-//   relu keeps it).
+//   instruction per 2 elements instead of a v_max_f32 per element.  NaNs: a positive-sign NaN stays
+//   NaN (as torch.relu keeps it), a NEGATIVE-sign NaN (e.g. 0xFFC0) is a negative int16 and becomes
+//   +0 -- the one input class where this differs from torch.relu.
 PIPNET_DEV void add_bf16x8(f32x4& x0, f32x4& x1, const bf16x8& r) {
   const u32x4 u = __builtin_bit_cast(u32x4, r);
   const u32x4 ev = u << 16, od = u & 0xffff0000u;   // elements 2j (low half) / 2j + 1 (high half)

@@ -705,7 +705,34 @@ __global__ void seed_advance_kernel(uint64_t* seed) {
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   seed[1] = z ^ (z >> 31);
 }
+// The head's noise draw on its own: element i of a [n] stream (n % 4 == 0) = the Exp(1) value
+// (log_e = 0: exp1_from_bits, the soft / injected-form libm draw) or its log on the hard head's
+// hardware-log form (log_e = 1: log_exp1_from_bits_fast) of word i % 4 of Philox block offset + i / 4
+// -- exactly what count_gumbel_kernel consumes for element i of its NHWC [B, HW, P] map.
+__global__ __launch_bounds__(256) void philox_exp1_kernel(uint64_t seed, uint64_t offset, int64_t nblk, int log_e,
+                                                          float* __restrict__ out) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nblk; q += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t w[4];
+    philox4(seed, offset + (uint64_t)q, w);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = log_e ? log_exp1_from_bits_fast(w[e]) : exp1_from_bits(w[e]);
+    st4(out + 4 * q, o);
+  }
+}
 }  // namespace
+
+extern "C" int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e, float* out, void* stream) {
+  if (n < 0 || (n & 3) || (log_e != 0 && log_e != 1) || (n > 0 && !out)) return PIPNET_ERR_ARG;
+  if (!aligned16(out)) return PIPNET_ERR_ALIGN;
+  if (n == 0) return PIPNET_OK;
+  const int64_t nblk = n / 4;
+  const int64_t g = (nblk + 255) / 256;
+  hipLaunchKernelGGL(philox_exp1_kernel, dim3((unsigned)(g < 16384 ? g : 16384)), dim3(256), 0, (hipStream_t)stream,
+                     seed, offset, nblk, log_e, out);
+  PIPNET_CHECK_LAUNCH();
+  return PIPNET_OK;
+}
 
 extern "C" int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau, const float* exp_noise,
                                        uint64_t seed, uint64_t offset, float* proto, int32_t* hist, void* stream) {

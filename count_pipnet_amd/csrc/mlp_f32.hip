@@ -301,15 +301,23 @@ __device__ __forceinline__ void cnblock_mlp_body(const float* __restrict__ t, co
   }
 }
 
+// Occupancy: HIP's second __launch_bounds__ argument is min WAVES PER EU (amdgpu_waves_per_eu), not
+// workgroups per CU, so the target is stated directly: two waves per SIMD (a 256-register budget)
+// for the 2- and 4-wave workgroups, one for the 8-wave forms, the 1-wave forms and C = 192 / HC = 32
+// (their LDS allows fewer than 8 waves per CU anyway).  (The former `8 / NW` asked NW = 1 / 2 for 8 / 4 waves
+// per EU; LLVM clipped that to the LDS-bound occupancy, so no kernel spilled -- tools/isa_dump.sh
+// mlp_f32 shows scratch 0 for every instantiation either way.)
+constexpr int mlp_waves_per_eu(int C, int HC, int NW) { return (NW >= 8 || NW == 1 || (C == 192 && HC == 32)) ? 1 : 2; }
+#define PIPNET_MLP_BOUNDS(NW) __launch_bounds__(64 * (NW)) __attribute__((amdgpu_waves_per_eu(mlp_waves_per_eu(C, HC, NW))))
 template <int C, int HC, int NW, int PX, int HS = 1>
-__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_kernel(
+__global__ PIPNET_MLP_BOUNDS(NW) void cnblock_mlp_kernel(
     const float* __restrict__ t, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma, float* x, int M) {
   cnblock_mlp_body<C, HC, NW, PX, HS, 0>(t, W1, b1, W2, b2, gamma, x, M);
 }
 
 template <int C, int HC, int NW, int PX, int HS, int ABL>   // tuning lab only (tools/mlp_lab.hip)
-__global__ __launch_bounds__(64 * NW, NW >= 8 ? 1 : 8 / NW) void cnblock_mlp_abl_kernel(
+__global__ PIPNET_MLP_BOUNDS(NW) void cnblock_mlp_abl_kernel(
     const float* __restrict__ t, const float* __restrict__ W1, const float* __restrict__ b1,
     const float* __restrict__ W2, const float* __restrict__ b2, const float* __restrict__ gamma, float* x, int M) {
   cnblock_mlp_body<C, HC, NW, PX, HS, ABL>(t, W1, b1, W2, b2, gamma, x, M);

@@ -30,14 +30,20 @@ PIPNET_DEV void philox4(uint64_t seed, uint64_t ctr, uint32_t (&out)[4]) {
   out[0] = c0, out[1] = c1, out[2] = c2, out[3] = c3;
 }
 
+// E = -log u of the word's top 24 bits, u = (k + 1/2) 2^-24.  In fp32 the top value k = 2^24 - 1
+// rounds to u = 1.0 (16777215.5 needs 25 bits; ties to even), so E would be 0 and log E = -inf --
+// the soft head's z = +inf and its softmax NaN, once in 2^24 draws.  E is floored at
+// 2^-25 (below every other draw's value, >= 8.9e-8), which changes only that one case.
+// oracle/philox_ref.py restates this draw.
 PIPNET_DEV float exp1_from_bits(uint32_t w) {
-  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
-  return -logf(u);
+  const float u = ((float)(w >> 8) + 0.5f) * (1.0f / 16777216.0f);   // (0, 1]
+  return fmaxf(-logf(u), 2.98023224e-8f);
 }
 
 // log E for E = -log u of the same 24-bit uniform, on the hardware log2 (v_log_f32):
-// ln E = ln2 * log2(-log2 u) + ln(ln2).  u lies in [2^-25, 1 - 2^-25], so -log2 u >= 2^-25 / ln2;
-// v_log_f32 returns 0 for u within a few ulp of 1, which made log E = -inf, z = +inf and the
+// ln E = ln2 * log2(-log2 u) + ln(ln2).  The same floor E >= 2^-25, i.e. -log2 u >= 2^-25 / ln2;
+// v_log_f32 returns 0 for u within a few ulp of 1 (and u = 1.0 exactly, above), which made log E =
+// -inf, z = +inf and the
 // pixel's one-hot value NaN (inf - inf in the exp-sum) about twice per C5 forward -- the inner
 // value is clamped to that bound (every other draw unchanged).  For the hard Philox head only --
 // its noise is this library's own draw; the injected-noise and soft paths keep the libm forms

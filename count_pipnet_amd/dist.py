@@ -8,8 +8,10 @@ gathers all three outputs back to GPU 0.  Here:
   * weights are loaded once per device (each rank owns a resident replica);
   * the global batch is split exactly like ``DataParallel.scatter`` (``torch.chunk`` along
     dim 0, so shard sizes and order match), or each rank passes its own shard;
-  * the only exchange is one all-gather of ``pooled`` [B/N, P] and ``out`` [B/N, K]
-    over RCCL/xGMI -- no reduction is needed because images are independent (SURVEY.md 8e);
+  * the only exchange is ONE all-gather of ``pooled`` [B/N, P] and ``out`` [B/N, K] packed side
+    by side into one [B/N, P + K] buffer over RCCL/xGMI (the exchange is latency-bound, tens of us
+    per collective, so one collective instead of two halves it) -- no reduction is needed because
+    images are independent (SURVEY.md 8e);
   * ``proto_features`` is gathered to rank 0 when the caller uses DataParallel's call
     pattern (the full batch on every rank): DataParallel gathers all three outputs to
     ``device_ids[0]`` and callers index ``proto_features[i]`` across the batch
@@ -99,6 +101,9 @@ class ShardedInference(nn.Module):
         self.module = module
         self.process_group = process_group
         self.gather_proto = gather_proto
+        # bench.py: when a list, every forward appends the (start, end) HIP events bracketing its
+        # pooled + logits exchange on the current stream (the collective's cost per step)
+        self.exchange_events: Optional[list] = None
 
     @property
     def world(self) -> int:
@@ -137,8 +142,7 @@ class ShardedInference(nn.Module):
             else:
                 sizes = [local.shape[0]]
         proto, pooled, out = self.module(local, inference=inference)
-        pooled = all_gather_rows(pooled, sizes, self.process_group)
-        out = all_gather_rows(out, sizes, self.process_group)
+        pooled, out = exchange_outputs(pooled, out, sizes, self.process_group, self.exchange_events)
         if world > 1:
             if self.gather_proto is None and global_batch:
                 proto = gather_proto_features(proto, sizes, self.process_group, to_root=True)
@@ -147,6 +151,30 @@ class ShardedInference(nn.Module):
             elif self.gather_proto:
                 proto = gather_proto_features(proto, sizes, self.process_group)
         return proto, pooled, out
+
+
+def exchange_outputs(pooled: Tensor, out: Tensor, sizes: List[int], group=None,
+                     events: Optional[list] = None) -> Tuple[Tensor, Tensor]:
+    """All-gather this rank's ``pooled`` [b, P] and ``out`` [b, K] rows in ONE collective: both
+    are written side by side into a [b, P + K] buffer (same dtype), gathered with one
+    ``all_gather_into_tensor`` and split back into contiguous [B, P] / [B, K] tensors in global
+    batch order.  ``events``: a list that receives the (start, end) events of the exchange."""
+    if len(sizes) == 1:
+        return pooled, out
+    if pooled.dtype != out.dtype:
+        raise RuntimeError(f"exchange_outputs: pooled {pooled.dtype} and logits {out.dtype} differ")
+    e0 = e1 = None
+    if events is not None and pooled.is_cuda:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+    p = pooled.shape[1]
+    both = torch.cat([pooled, out], dim=1)
+    g = all_gather_rows(both, sizes, group)
+    pooled_g, out_g = g[:, :p].contiguous(), g[:, p:].contiguous()
+    if e1 is not None:
+        e1.record()
+        events.append((e0, e1))
+    return pooled_g, out_g
 
 
 def gather_proto_features(proto: Tensor, sizes: List[int], group=None, to_root: bool = False) -> Tensor:

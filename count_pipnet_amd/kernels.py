@@ -6,6 +6,8 @@ streams, events and graph capture.  Nothing here computes on the host.
 """
 from __future__ import annotations
 
+import functools
+
 from typing import Optional, Tuple
 
 import os
@@ -261,38 +263,34 @@ def _chk_bf(t: Tensor, what: str) -> None:
         raise RuntimeError(f"count_pipnet_amd: {what} must be contiguous")
 
 
-def bf16_conv_tile(m: int, n: int, pp_ok: bool = True, s3: bool = False, kv: int = 0, halo_ok: bool = False,
-                   ppp_ok: bool = False, halo64_ok: bool = False) -> int:
-    """Workgroup tile the library picks (mirrors conv_variant / launch_conv in csrc/conv_bf16.hip):
+@functools.lru_cache(maxsize=4096)
+def bf16_conv_plan(b: int, h: int, w: int, cin: int, cout: int, kh: int, kw: int, stride: int, pad: int,
+                   epilogue: int, tile: int = -1) -> int:
+    """The workgroup tile the library takes for this bf16 conv (pipnet_conv2d_nhwc_bf16_plan: the
+    library's own rule, csrc/conv_bf16.hip plan_conv -- never mirrored here):
     9 = the persistent ping-pong tile (1x1 stride-1 convs with N % 256 == 0, plain epilogues),
-    11 = 3x3 stride-1 pad-1 Cin = N = 64 (W <= 63) / 128 (W <= 31) convs on an LDS input halo (the
-    arithmetic of tiles 6 / 4),
+    11 = 3x3 stride-1 pad-1 Cin = N = 64 (W <= 63) / 128 (W <= 31) convs on an LDS input halo,
     8 = the ping-pong tile with an LDS input halo (3x3 stride-1 pad-1, Cin % 64 == 0, W <= 31, N >= 256),
-    5 = 256x256 ping-pong on 16x16x32 MFMAs (every other N >= 256 layer with Cin % 32 == 0, any M),
-    6 = 256x64 (N <= 64), else 0 = 64x128, 3 = 256x256, 4 = 128x128 -- all but 5 / 8 / 9 on
-    32x32x16 MFMAs with 32-deep K tiles in 4 LDS stages, so the K order never depends on M.
-    ``kv`` = KH*KW*Cin: layers with K <= 64 never take the single-workgroup ping-pong tiles."""
-    if s3:
-        m128 = 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
-        if not pp_ok:
-            return m128
-        if n == 192:
-            return 7
-        if n == 384:
-            return 7 if kv >= 3 * 1024 else m128
-        return 5 if n >= 256 else m128
-    if halo_ok:
-        return 8
-    if halo64_ok:
-        return 11
-    short_k = 0 < kv <= 64                  # layer1 conv3 / downsample (K = 64): 2-workgroup tiles
-    if n >= 256 and pp_ok and not short_k:
-        return 9 if ppp_ok else 5
-    if n <= 64 and not s3:
-        return 6
-    if n >= 256 and -(-m // 256) * -(-n // 256) >= 256 and not short_k:
-        return 3
-    return 4 if -(-m // 128) * -(-n // 128) >= 256 else 0
+    5 = 256x256 ping-pong on 16x16x32 MFMAs, 6 = 256x64 (N <= 64), 0 = 64x128, 3 = 256x256,
+    4 = 128x128.  ``tile`` >= 0 is validated instead of chosen."""
+    v = _lib.load().pipnet_conv2d_nhwc_bf16_plan(b, h, w, cin, cout, kh, kw, stride, pad, epilogue, tile)
+    if v < 0:
+        raise RuntimeError(f"conv2d_nhwc_bf16: no tile {tile} for {b}x{h}x{w}x{cin} -> {cout} k{kh}x{kw} s{stride} "
+                           f"p{pad} epilogue {epilogue}")
+    return v
+
+
+def s3_conv_tile(m: int, n: int, pp_ok: bool = True, kv: int = 0) -> int:
+    """Tile of a split-bf16 GEMM (csrc/conv_bf16.hip conv_variant's s3 branch; tiles 0 / 4 / 5 / 7).
+    The split path's labels only -- the ResNet bf16 convs ask the library (bf16_conv_plan)."""
+    m128 = 4 if -(-m // 128) * -(-n // 128) >= 512 else 0
+    if not pp_ok:
+        return m128
+    if n == 192:
+        return 7
+    if n == 384:
+        return 7 if kv >= 3 * 1024 else m128
+    return 5 if n >= 256 else m128
 
 
 _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cfg<2, 2, 2, 2, 64, 2>", 2),
@@ -303,11 +301,10 @@ _BF16_CFG = {0: ("pipnet_bf16::Cfg<2, 2, 1, 2, 32, 4>", 3), 1: ("pipnet_bf16::Cf
 PP_RB = 8     # row blocks of the 256-wide ping-pong tiles (csrc/conv_bf16.hip PP_RB): 256-row tiles
 
 
-def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int = -1, pp_ok: bool = True,
-                          s3: bool = False, kv: int = 0, halo_ok: bool = False, ppp_ok: bool = False,
-                          halo64_ok: bool = False) -> str:
-    """rocprof name of the bf16 conv instantiation."""
-    t = bf16_conv_tile(m, n, pp_ok, s3, kv, halo_ok, ppp_ok, halo64_ok) if tile < 0 else tile
+def bf16_conv_kernel_name(m: int, n: int, epilogue: int, aload: int, tile: int, s3: bool = False,
+                          kv: int = 0) -> str:
+    """rocprof name of the bf16 conv instantiation of ``tile`` (bf16_conv_plan / s3_conv_tile)."""
+    t = tile
     if t == 11:
         return f"pipnet_bf16::conv3x3_bf16_hsmall_kernel<{kv // 9}, {epilogue}>"
     if t == 9:
@@ -361,20 +358,10 @@ def conv2d_nhwc_bf16(x: Tensor, w_packed: Tensor, kh: int, kw: int, bias: Option
     y = torch.empty((b, oh, ow, cout), device=x.device, dtype=torch.bfloat16)
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
-    pp_ok = (aload == 0 or cin % 32 == 0) and kp % 32 == 0
-    halo_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin % 64 == 0 and w <= 31 and cout >= 256
-               and b * h * w * cin < 2 ** 31          # conv_bf16.hip halo_ok: 32-bit halo source offsets
-               and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    ppp_ok = (aload == 0 and pp_ok and cout % 256 == 0
-              and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    halo64_ok = (kh == 3 and kw == 3 and stride == 1 and pad == 1 and cin == cout
-                 and ((cin == 64 and w <= 63) or (cin == 128 and w <= 31))
-                 and epilogue in (_lib.EPI_NONE, _lib.EPI_BIAS, _lib.EPI_BIAS_RELU, _lib.EPI_BIAS_RESID_RELU))
-    if halo64_ok and tile < 0 and not CONV3X3_N64_HALO:
-        halo64_ok = False                   # the same arithmetic on the generic tile
-        tile = 6 if cout == 64 else bf16_conv_tile(m, cout, pp_ok, kv=k)
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, pp_ok, kv=k, halo_ok=halo_ok, ppp_ok=ppp_ok,
-                                  halo64_ok=halo64_ok),
+    if tile < 0 and not CONV3X3_N64_HALO and bf16_conv_plan(b, h, w, cin, cout, kh, kw, stride, pad, epilogue) == 11:
+        tile = 6 if cout == 64 else 4       # the same arithmetic on the generic tile (A/B arm)
+    t = bf16_conv_plan(b, h, w, cin, cout, kh, kw, stride, pad, epilogue, tile)
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, t, kv=k),
             2.0 * m * cout * k,
             lambda: _lib.call("pipnet_conv2d_nhwc_bf16_tile", x.data_ptr(), b, h, w, cin, w_packed.data_ptr(),
                               _ptr(bias), cout, kh, kw, stride, pad, _ptr(r), epilogue, y.data_ptr(), tile,
@@ -602,7 +589,8 @@ def conv_s3(x2: Tensor, w_packed: Tensor, kh: int, kw: int, cout: int, bias: Opt
         raise RuntimeError(f"conv_s3: out {tuple(out.shape)} {out.dtype} does not match {shape} {dt}")
     m = b * oh * ow
     aload = 0 if (kh == 1 and kw == 1 and stride == 1 and pad == 0) else 2
-    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, tile, True, s3=True, kv=k), 2.0 * m * cout * k / 3.0,
+    t = tile if tile >= 0 else s3_conv_tile(m, cout, kv=k)
+    _launch(bf16_conv_kernel_name(m, cout, epilogue, aload, t, s3=True, kv=k), 2.0 * m * cout * k / 3.0,
             lambda: _lib.call("pipnet_conv2d_nhwc_s3", x2.data_ptr(), b, h, w, cin, w_packed.data_ptr(), _ptr(bias),
                               _ptr(scale), _ptr(r), cout, kh, kw, stride, pad, epilogue, out.data_ptr(), tile,
                               _stream(x2)))
@@ -697,8 +685,10 @@ _HEAD_WS = {}
 
 def _head_workspace(dev: torch.device, stream: int, nfloats: int, b: int) -> Tuple[Tensor, Tensor]:
     key = (dev.index, stream)
-    part, tickets = _HEAD_WS.get(key, (None, None))
     capturing = torch.cuda.is_current_stream_capturing()
+    # a capture always takes graph-owned scratch: a cached eager buffer shared with the graph would
+    # race on its tickets when a replay on another stream runs beside an eager call
+    part, tickets = (None, None) if capturing else _HEAD_WS.get(key, (None, None))
     if part is None or part.numel() < nfloats:
         part = torch.zeros(max(nfloats, 4), device=dev, dtype=torch.float32)
     if tickets is None or tickets.numel() < b:
@@ -872,6 +862,19 @@ def count_head_backward(proto_nhwc: Tensor, counts: Tensor, d_counts: Optional[T
               _ptr(d_counts), float(w_align), float(w_tanh), float(tanh_coeff), 1.0 / float(tau), dcnt.data_ptr(),
               d_logits.data_ptr(), _stream(proto_nhwc))
     return d_logits
+
+
+def philox_exp1(seed: int, offset: int, n: int, device, log_e: bool = False) -> Tensor:
+    """The Gumbel heads' Exp(1) draw on its own (pipnet_philox_exp1_f32): element i = the value
+    count_gumbel uses for element i of its NHWC [B, HW, P] stream under (seed, offset) -- E, or
+    log E on the hard head's hardware-log form.  For parity tests (oracle/philox_ref.py)."""
+    if n % 4:
+        raise RuntimeError(f"philox_exp1: n = {n} must be a multiple of 4")
+    out = torch.empty(n, device=device, dtype=torch.float32)
+    _chk(out, "philox output")
+    _lib.call("pipnet_philox_exp1_f32", int(seed) & (2 ** 64 - 1), int(offset) & (2 ** 64 - 1), n, int(log_e),
+              out.data_ptr(), _stream(out))
+    return out
 
 
 def count_gumbel_devseed(logits_nhwc: Tensor, tau: float, seed_state: Tensor) -> Tuple[Tensor, Tensor]:

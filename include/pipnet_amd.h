@@ -52,7 +52,8 @@ extern "C" {
  * _stream / _bk16x3 / _plain_store, pipnet_conv_bf16_rb, pipnet_head_bf16_quads) and
  * pipnet_linear_agelu_f32 are gone -- kernel selection is a fixed per-shape rule with no
  * mutable library state -- and the one-launch fused head pipnet_softmax_pool_linear_f32 / _bf16
- * (+ _part_floats) and pipnet_matmul2_f64acc_f32 are new (round 5).  A caller built against an older version must not bind this library. */
+ * (+ _part_floats) and pipnet_matmul2_f64acc_f32 are new (round 5).  A caller built against an older version must not bind this library.
+ * Round 6 only ADDS entry points (pipnet_philox_exp1_f32, pipnet_conv2d_nhwc_bf16_plan); no signature changed. */
 #define PIPNET_AMD_ABI_VERSION 3
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -329,6 +330,20 @@ int pipnet_count_gumbel_f32(const float* logits, int B, int HW, int P, float tau
  * noise), so a captured hipGraph replays with new noise every time. */
 int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int HW, int P, float tau,
                                     uint64_t* seed_state, float* proto, int32_t* hist, void* stream);
+
+/* The Gumbel heads' Exp(1) noise on its own (parity tests; oracle/philox_ref.py restates it):
+ * out[i] for i < n (n % 4 == 0) = the draw count_gumbel_kernel uses for element i of its NHWC
+ * [B,HW,P] stream under (seed, offset): word i % 4 of Philox4x32-10 block offset + i/4, E = -log u
+ * with u = (top 24 bits + 1/2) 2^-24 floored at E >= 2^-25.  log_e = 0: E (the soft head's libm
+ * form); log_e = 1: log E on the hard head's hardware-log form.  Replaces the
+ * `-torch.empty_like(x).exponential_().log()` draw inside F.gumbel_softmax (count_pipnet_utils.py:36-38). */
+int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e, float* out, void* stream);
+
+/* bf16 conv tile plan: the tile id pipnet_conv2d_nhwc_bf16_tile takes for this shape / epilogue
+ * (tile -1 = the automatic choice, >= 0 validated), or -PIPNET_ERR_ARG.  The library's own rule,
+ * exported so that profiling labels never mirror it (kernels.bf16_conv_kernel_name). */
+int pipnet_conv2d_nhwc_bf16_plan(int B, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                                 int epilogue, int tile);
 
 /* Count finish (count_pipnet.py:88-97): counts_raw = float(hist) (or sums when hist is
  * NULL), clamped = clamp(round?(counts), 0, max_count) -- round when do_round.

@@ -77,7 +77,9 @@ def test_bench_self_launches_two_ranks(gpu):
     assert len(lines) == 1, r.stdout[-2000:]
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["global_batch"] == 128 and res["config"]["parallelism"] == "dp2"
-    assert res["config"]["exchange"] == "gloo all_gather(logits, pooled)"
+    ex = res["config"]["exchange"]
+    assert ex["collective"] == "gloo all_gather_into_tensor([pooled | logits])" and ex["collectives_per_step"] == 1
+    assert ex["ms_per_step"] is not None and ex["ms_per_step"] > 0
     assert res["config"]["num_classes"] == 200 and res["value"] > 0
 
 

@@ -104,10 +104,41 @@ def test_roofline_kernel_names_exist_in_library():
     assert K.cnblock_mlp_kernel_name(192, 16384, hw=256) in out          # hidden split (C5 stage 2)
     assert "pipnet_bf16::conv_bf16_ppp_kernel<12, 8>" in out                  # dual 1x1 (downsample + conv1)
     assert "pipnet_bf16::stem_pool_bf16_kernel" in out                     # fused stem + max-pool
-    for m, c in ((401408, 64), (100352, 128)):                               # small-N halo tile (11)
-        assert K.bf16_conv_kernel_name(m, c, _lib.EPI_BIAS_RELU, 2, kv=9 * c, halo64_ok=True) in out
-    for m, n, epi, s3 in [(200704, 96, _lib.EPI_F32_RESID, True), (200704, 384, _lib.EPI_S3_GELU, True),
-                          (50176, 192, _lib.EPI_F32_RESID, True), (401408, 64, _lib.EPI_BIAS_RELU, False),
-                          (100352, 128, _lib.EPI_BIAS_RELU, False)]:
-        name = K.bf16_conv_kernel_name(m, n, epi, 0, s3=s3)
-        assert name in syms, (m, n, epi, s3, name)
+    for m, n, epi in [(200704, 96, _lib.EPI_F32_RESID), (200704, 384, _lib.EPI_S3_GELU),
+                      (50176, 192, _lib.EPI_F32_RESID)]:                      # split-bf16 GEMMs
+        name = K.bf16_conv_kernel_name(m, n, epi, 0, K.s3_conv_tile(m, n, kv=3 * 4 * n), s3=True)
+        assert name in syms, (m, n, epi, name)
+
+
+# The C3 ResNet-50 bf16 layer list at 64 images of 224^2 (resnet_hip.py's launches):
+# (name, H_in, Cin, Cout, k, stride, pad, epilogue, expected tile)
+C3_LAYERS = [
+    ("l1.c1", 56, 64, 64, 1, 1, 0, _lib.EPI_BIAS_RELU, 6), ("l1.c2", 56, 64, 64, 3, 1, 1, _lib.EPI_BIAS_RELU, 11),
+    ("l1.c3", 56, 64, 256, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU, 4), ("l1.ds", 56, 64, 256, 1, 1, 0, _lib.EPI_BIAS, 4),
+    ("l1.c1b", 56, 256, 64, 1, 1, 0, _lib.EPI_BIAS_RELU, 6),
+    ("l2.c1", 56, 256, 128, 1, 1, 0, _lib.EPI_BIAS_RELU, 4), ("l2.c2s", 56, 128, 128, 3, 2, 1, _lib.EPI_BIAS_RELU, 4),
+    ("l2.c2", 28, 128, 128, 3, 1, 1, _lib.EPI_BIAS_RELU, 11),
+    ("l2.c3", 28, 128, 512, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU, 9), ("l2.ds", 56, 256, 512, 1, 2, 0, _lib.EPI_BIAS, 5),
+    ("l3.c1", 28, 512, 256, 1, 1, 0, _lib.EPI_BIAS_RELU, 9), ("l3.c2", 28, 256, 256, 3, 1, 1, _lib.EPI_BIAS_RELU, 8),
+    ("l3.c3", 28, 256, 1024, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU, 9),
+    ("l4.c1", 28, 1024, 512, 1, 1, 0, _lib.EPI_BIAS_RELU, 9), ("l4.c2", 28, 512, 512, 3, 1, 1, _lib.EPI_BIAS_RELU, 8),
+    ("l4.c3", 28, 512, 2048, 1, 1, 0, _lib.EPI_BIAS_RESID_RELU, 9),
+]
+
+
+def test_bf16_labels_come_from_the_library_plan():
+    """The roofline / profiling label of every C3 conv is the library's own tile choice
+    (pipnet_conv2d_nhwc_bf16_plan, no Python mirror), and names a kernel instantiated in the library."""
+    from count_pipnet_amd import kernels as K
+    build.build()
+    out = _nm_demangled()
+    for name, h, cin, cout, k, s, pad, epi, want in C3_LAYERS:
+        t = K.bf16_conv_plan(64, h, h, cin, cout, k, k, s, pad, epi)
+        assert t == want, (name, t, want)
+        oh = (h + 2 * pad - k) // s + 1
+        label = K.bf16_conv_kernel_name(64 * oh * oh, cout, epi, 0 if k == 1 and s == 1 else 2, t, kv=k * k * cin)
+        assert label in out, (name, label)
+    # a requested tile is validated, not chosen: tile 8 needs a 3x3 stride-1 halo shape
+    import pytest
+    with pytest.raises(RuntimeError):
+        K.bf16_conv_plan(64, 56, 56, 256, 512, 1, 1, 2, 0, _lib.EPI_BIAS, 8)

@@ -135,3 +135,62 @@ def test_sharded_inference_two_groups_world8():
         p.join(timeout=300)
     res = dict(q.get(timeout=5) for _ in range(8))
     assert res == {r: True for r in range(8)}
+
+
+def _one_collective_worker(rank, world, port, q):
+    """One forward of the per-rank shard call (bench.py's) issues exactly ONE collective -- the
+    packed [b, P + K] all-gather of pooled and logits -- and its outputs equal the single-process
+    full-batch forward (pooled / logits split back out of the packed rows, contiguous)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+        from count_pipnet_amd.backend import torch_backend
+        from golden_util import golden_inputs, load_golden
+        from model_util import build_model
+        meta, _ = load_golden("pipnet_mid_addon")
+        net = build_model(meta)
+        xs = torch.cat([golden_inputs(meta)] * 2)[:4]
+        sizes = shard_sizes(4, world)
+        start = sum(sizes[:rank])
+        calls = []
+        names = ("all_gather_into_tensor", "all_gather", "gather", "all_reduce", "broadcast", "reduce_scatter",
+                 "all_to_all", "all_to_all_single")
+        orig = {n: getattr(dist, n) for n in names}
+
+        def counted(n):
+            def f(*a, **k):
+                calls.append(n)
+                return orig[n](*a, **k)
+            return f
+        wrapped = ShardedInference(net, gather_proto=False)
+        with torch.no_grad(), torch_backend():
+            _, r_pooled, r_out = net(xs, inference=True)
+            for n in names:
+                setattr(dist, n, counted(n))
+            try:
+                _, pooled, out = wrapped(xs[start:start + sizes[rank]], inference=True, global_batch=False,
+                                         sizes=sizes)
+            finally:
+                for n in names:
+                    setattr(dist, n, orig[n])
+        ok = (calls == ["all_gather_into_tensor"] and pooled.is_contiguous() and out.is_contiguous()
+              and torch.allclose(pooled, r_pooled, atol=1e-6) and torch.allclose(out, r_out, rtol=1e-5, atol=1e-5))
+        q.put((rank, bool(ok), calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_one_collective_per_forward_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_one_collective_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    res = {r: (ok, calls) for r, ok, calls in (q.get(timeout=5) for _ in range(2))}
+    assert all(ok for ok, _ in res.values()), res

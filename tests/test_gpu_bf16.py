@@ -126,7 +126,7 @@ def test_conv_bf16_halo(gpu, b, cin, cout, h, w, epi):
     ref = _bf(y.float()).permute(0, 2, 3, 1)
     nhwc = lambda t: t.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).to(gpu)  # noqa: E731
     wp = K.pack_conv_weight_bf16(wt.permute(0, 2, 3, 1).contiguous().to(gpu))
-    assert K.bf16_conv_tile(b * h * w, cout, halo_ok=True) == 8
+    assert K.bf16_conv_plan(b, h, w, cin, cout, 3, 3, 1, 1, epi) == 8
     outs = [K.conv2d_nhwc_bf16(nhwc(x), wp, 3, 3, bias.float().to(gpu) if epi != _lib.EPI_NONE else None, 1, 1, epi,
                                nhwc(r) if epi == _lib.EPI_BIAS_RESID_RELU else None, tile=t) for t in (-1, 8)]
     torch.cuda.synchronize()

@@ -63,10 +63,7 @@ def main():
               else None for _ in range(a.rotate)]
         x, r = xs[0], rs[0]
         flops = 2.0 * a.batch * oh * oh * cout * k * k * cin
-        halo = k == 3 and s == 1 and pad == 1 and cin % 64 == 0 and oh <= 31 and cout >= 256
-        ppp = k == 1 and s == 1 and pad == 0 and cout % 256 == 0
-        h64 = k == 3 and s == 1 and pad == 1 and cin == cout and ((cin == 64 and oh <= 63) or (cin == 128 and oh <= 31))
-        auto = K.bf16_conv_tile(a.batch * oh * oh, cout, kv=k * k * cin, halo_ok=halo, ppp_ok=ppp, halo64_ok=h64)
+        auto = K.bf16_conv_plan(a.batch, h, h, cin, cout, k, k, s, pad, epi)
         line = f"{name:8s} M={a.batch * oh * oh:6d} N={cout:4d} K={k * k * cin:5d} auto={auto}"
         for t in tiles:
             ti = t
