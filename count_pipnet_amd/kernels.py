@@ -643,7 +643,9 @@ def softmax_pool_linear(feat_nhwc: Tensor, w: Tensor, bias: Optional[Tensor], th
     (proto [B,h,w,P], pooled [B,P], x' [B,P], logits [B,K]) with x' = where(pooled < thresh, 0,
     pooled) (or pooled when ``thresh`` is None) and logits = x' relu(w)^T + bias, w read at call
     time.  ``out`` = (proto, pooled, x', logits) to write into (batch slices of a larger output).
-    Bitwise equal to softmax_pool(..., 0) + nonneg_linear."""
+    Bitwise equal to softmax_pool(..., 0) + nonneg_linear.  Under HIP-graph capture the call keeps
+    using the capture stream's cached scratch (one graph node): serialise replays with eager calls
+    on that stream."""
     bf = feat_nhwc.dtype == torch.bfloat16
     if bf:
         _chk_bf(feat_nhwc, "prototype logits")
@@ -685,10 +687,13 @@ _HEAD_WS = {}
 
 def _head_workspace(dev: torch.device, stream: int, nfloats: int, b: int) -> Tuple[Tensor, Tensor]:
     key = (dev.index, stream)
+    # A capture reuses this stream's cached scratch when it is large enough (so the captured head
+    # stays ONE graph node: a graph-owned buffer would add its zero-fill nodes).  The graph then
+    # shares the scratch -- and its self-resetting tickets -- with eager calls on the capture
+    # stream: replays must be serialised with such calls (replay on the capture stream, or
+    # synchronise first); a replay on another stream racing an eager call would corrupt both.
+    part, tickets = _HEAD_WS.get(key, (None, None))
     capturing = torch.cuda.is_current_stream_capturing()
-    # a capture always takes graph-owned scratch: a cached eager buffer shared with the graph would
-    # race on its tickets when a replay on another stream runs beside an eager call
-    part, tickets = (None, None) if capturing else _HEAD_WS.get(key, (None, None))
     if part is None or part.numel() < nfloats:
         part = torch.zeros(max(nfloats, 4), device=dev, dtype=torch.float32)
     if tickets is None or tickets.numel() < b:
