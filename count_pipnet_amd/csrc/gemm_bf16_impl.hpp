@@ -491,6 +491,26 @@ PIPNET_DEV void pp_barrier() {
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
+// ds_read_b128 the compiler does not track (its waitcnt pass sees the value as ready at issue):
+// the caller waits with lgkm_wait_dyn before the first use
+PIPNET_DEV bf16x8v ds_read_b128_asm(const unsigned char* p) {
+  bf16x8v v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+template <int N>
+PIPNET_DEV void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
+PIPNET_DEV void lgkm_wait_dyn(int n) {        // n compile-time after unrolling
+  switch (n) {
+    case 0: lgkm_wait<0>(); break;
+    case 1: lgkm_wait<1>(); break;
+    case 2: lgkm_wait<2>(); break;
+    default: lgkm_wait<3>(); break;
+  }
+}
 
 // Epilogue of the 256-row ping-pong tiles: per row half, the wave's fp32 accumulators are
 // re-laid through its own LDS rows (64 x 68 floats), then every lane finishes 8 consecutive
@@ -1087,7 +1107,13 @@ struct Lay {
 // epilogue (one store per lane keeps the accumulators live), 4 = no barriers, 8 = no A fragment
 // reads after the first, 16 = no halo DMA after pair 0 (stale LDS / registers: timing only).
 // (The body is a device function so that the product kernel's name carries no lab parameter.)
-template <int EPI, int NB, int RB, int ABL>
+// SEG = MFMA segments per 32-deep K-tile: 2 = two 16-MFMA phases (row halves), each between a
+// barrier pair (rounds 2-5); 1 = ONE 32-MFMA segment per K-tile (round 6): the R segment issues
+// the DMA, reads B and the row-half-0 A fragments and does the counted wait; the M segment runs
+// half 0's 16 MFMAs with half 1's four A-fragment reads interleaved (each refills the registers of
+// the row whose MFMAs just issued), then half 1's 16 -- half the barriers and priority switches per
+// MFMA, the same registers, and the same per-accumulator K order (bitwise equal).
+template <int EPI, int NB, int RB, int ABL, int SEG = 2>
 __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
   using namespace pp;
   using ph::NS;
@@ -1230,6 +1256,15 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
   };
   bf16x8v fa[4], fb[NB];
   const int lrow = wr * 16 * RB + fr;
+  // one A fragment row j (0..RB*2-1 of the wave group's 16-row blocks) for the SEG = 1 interleave
+  auto read_a_row = [&](bf16x8v& f, const unsigned char* hb, int j, int loff, unsigned tbit) {
+    if constexpr ((ABL & 8) != 0) {
+      if (a_once) return;
+    }
+    const unsigned char* ptr = (vmask[j] & tbit) ? hb + loff + j * 1024 : zb + (loff & 255);
+    if constexpr (SEG == 3) f = ds_read_b128_asm(ptr);      // waited for explicitly (below)
+    else f = *reinterpret_cast<const bf16x8v*>(ptr);
+  };
   int kt = 0;
   for (int P = 0; P < npair; ++P) {
     const bool more = P + 1 < npair;
@@ -1244,6 +1279,49 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
       for (int h = 0; h < 2; ++h, ++kt) {
         const unsigned char* st = smem + (kt & (NS - 1)) * L::BSTAGE;
         const unsigned char* hb = hp + h * L::HALO_BYTES;
+        if constexpr (SEG == 1 || SEG == 3) {
+          // ---- R segment: DMA (B of kt+2; the next pair's halo at (t, h) = (0, 1)), B and
+          // row-half-0 A fragments, wait for this wave's pieces of K-tile kt+1 ----
+          if (!last) stage_b(kt + 2);
+          if (h == 1 && t == 0 && more) stage_halo(P + 1);
+          read_b(fb, st);
+          read_a(fa, hb, 0, loff, tbit);
+          if (last) pp_wait_vm<0>();
+          else if (more && ((h == 1 && t == 0) || (h == 0 && t == 1))) pp_wait_vm<L::BPW + L::HPW>();
+          else pp_wait_vm<L::BPW>();
+          hbar();
+          // ---- M segment: 16 MFMAs of half 0 with half 1's A reads interleaved, 16 of half 1 ----
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int n = 0; n < NB; ++n)
+              acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+            if (r < RB - 4) {
+              __builtin_amdgcn_sched_barrier(0);
+              read_a_row(fa[r], hb, 4 + r, loff, tbit);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+          if constexpr ((ABL & 8) != 0) a_once = true;
+#pragma unroll
+          for (int r = 0; r < RB - 4; ++r) {
+            if constexpr (SEG == 3) {
+              // the compiler sees the inline-asm reads as ready at issue: wait for row r's own read
+              // only (LDS returns in order; the LDS-DMA in the loop makes the compiler's own waits
+              // lgkmcnt(0), which would stall on the last of the four reads)
+              __builtin_amdgcn_sched_barrier(0);
+              lgkm_wait_dyn(RB - 5 - r);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int n = 0; n < NB; ++n)
+              acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+          }
+          __builtin_amdgcn_s_setprio(0);
+          hbar();
+          continue;
+        }
         // ---- phase 0: rows 0..63 of the wave's block ----
         if (!last) stage_b(kt + 2);
         read_b(fb, st);
@@ -1297,9 +1375,9 @@ __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams
   conv3x3_bf16_halo_body<EPI, NB, RB, 0>(p);
 }
 
-template <int EPI, int NB, int RB, int ABL>   // tuning lab only (tools/bf16_lab.hip lab_halo)
+template <int EPI, int NB, int RB, int ABL, int SEG = 2>   // tuning lab only (tools/bf16_lab.hip lab_halo)
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_abl_kernel(ConvParams p) {
-  conv3x3_bf16_halo_body<EPI, NB, RB, ABL>(p);
+  conv3x3_bf16_halo_body<EPI, NB, RB, ABL, SEG>(p);
 }
 
 // ======================================================================================

@@ -746,13 +746,24 @@ extern "C" int lab_halo(int abl, const void* x, int B, int H, int W, int Cin, co
   hipStream_t s = (hipStream_t)stream;
 #define HALO_CASE(X) \
   case X: hipLaunchKernelGGL((conv3x3_bf16_halo_abl_kernel<PIPNET_EPI_NONE, 4, 8, X>), grid, dim3(512), 0, s, p); break;
+  // 1000 + bits: the one-segment-per-K-tile schedule (SEG = 1, round 6)
+#define HALO1_CASE(X) \
+  case 1000 + X: hipLaunchKernelGGL((conv3x3_bf16_halo_abl_kernel<PIPNET_EPI_NONE, 4, 8, X, 1>), grid, dim3(512), 0, s, p); break;
+  // 3000 + bits: SEG = 1 with the half-1 A reads as inline asm and explicit per-row lgkmcnt waits
+#define HALO3_CASE(X) \
+  case 3000 + X: hipLaunchKernelGGL((conv3x3_bf16_halo_abl_kernel<PIPNET_EPI_NONE, 4, 8, X, 3>), grid, dim3(512), 0, s, p); break;
   switch (abl) {
     case 0: hipLaunchKernelGGL((conv3x3_bf16_halo_kernel<PIPNET_EPI_NONE, 4, 8>), grid, dim3(512), 0, s, p); break;
     HALO_CASE(1) HALO_CASE(2) HALO_CASE(4) HALO_CASE(8) HALO_CASE(16) HALO_CASE(3) HALO_CASE(17)
     HALO_CASE(19) HALO_CASE(10) HALO_CASE(12) HALO_CASE(27)
+    HALO1_CASE(0) HALO1_CASE(1) HALO1_CASE(2) HALO1_CASE(4) HALO1_CASE(8) HALO1_CASE(16) HALO1_CASE(3)
+    HALO1_CASE(17) HALO1_CASE(19) HALO1_CASE(27)
+    HALO3_CASE(0) HALO3_CASE(2) HALO3_CASE(19) HALO3_CASE(3)
     default: return 1;
   }
 #undef HALO_CASE
+#undef HALO1_CASE
+#undef HALO3_CASE
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 

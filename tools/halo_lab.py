@@ -1,7 +1,8 @@
 """Time breakdown of the 3x3 LDS-halo ping-pong conv (conv3x3_bf16_halo_kernel, C3's dominant kernel) by
 ablation (tools/bf16_lab.hip lab_halo; ABL bits 1 = no B DMA, 2 = no epilogue, 4 = no barriers, 8 = no A
-fragment reads, 16 = no halo DMA), on the layer3 / layer4 conv2 shapes at the two-stream half batch and
-the full batch.  Variant 0 is the product kernel (checked bitwise against the library's tile 8).
+fragment reads, 16 = no halo DMA; 1000 + bits = the one-32-MFMA-segment-per-K-tile schedule, SEG = 1), on the
+layer3 / layer4 conv2 shapes at the two-stream half batch and the full batch.  Variants 0 / 1000 are full
+kernels (checked bitwise against the library's tile 8).
 
     python tools/halo_lab.py            (HALO_VARIANTS=0,1,2,... HALO_ROUNDS=3)
 """
@@ -27,7 +28,7 @@ def main():
     lib = bf16_lab.build()
     P, I = ctypes.c_void_p, ctypes.c_int
     lib.lab_halo.argtypes = [I, P, I, I, I, I, P, I, P, P]
-    variants = [int(v) for v in os.environ.get("HALO_VARIANTS", "0,1,2,4,8,16,3,17,19,10,12,27").split(",")]
+    variants = [int(v) for v in os.environ.get("HALO_VARIANTS", "0,1000,3000,2,1002,3002,19,1019,3019").split(",")]
     rounds = int(os.environ.get("HALO_ROUNDS", "3"))
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(0)
@@ -38,7 +39,7 @@ def main():
         y = torch.empty(b, hw, hw, n, device=dev, dtype=torch.bfloat16)
         ref = K.conv2d_nhwc_bf16(x, w, 3, 3, None, 1, 1, _lib.EPI_NONE, tile=8)
         same = {}
-        for v in (0,):                        # the product form: bitwise the library's tile 8
+        for v in [v for v in variants if v in (0, 1000, 3000)]:   # full (non-ablated) forms: bitwise the library's tile 8
             y.zero_()
             assert lib.lab_halo(v, x.data_ptr(), b, hw, hw, cin, w.data_ptr(), n, y.data_ptr(), stream) == 0
             torch.cuda.synchronize()
