@@ -512,6 +512,50 @@ PIPNET_DEV void lgkm_wait_dyn(int n) {        // n compile-time after unrolling
   }
 }
 
+// MFMA-segment schedule of the 256-row ping-pong tiles (halo 8, pp 5, persistent 9): 2 = two
+// 16-MFMA phases per 32-deep K-tile, each between a barrier pair (rounds 2-5); 3 = ONE 32-MFMA
+// segment per K-tile with the row-half-1 A reads interleaved as untracked (inline-asm) reads and
+// per-row lgkmcnt waits (round 6; profiles/r06/halo_seg_lab.txt).  Bitwise the same results: every
+// accumulator sees the same MFMA chain.  Build-time knobs for tools/ab_build.py A/B arms.
+#ifndef PIPNET_HALO_SEG
+#define PIPNET_HALO_SEG 3
+#endif
+#ifndef PIPNET_PP_SEG
+#define PIPNET_PP_SEG 3
+#endif
+#ifndef PIPNET_PPP_SEG
+#define PIPNET_PPP_SEG 3
+#endif
+
+// The SEG = 3 M segment: half 0's 4 x NB MFMAs, each row followed by the untracked read of the
+// half-1 fragment that reuses its registers, then half 1's (RB - 4) x NB MFMAs, each row after a
+// wait for its own read (LDS returns in order).  `rd(r)` returns half-1 row r's fragment through
+// ds_read_b128_asm.
+template <int RB, int NB, typename RD>
+PIPNET_DEV void pp_mseg3(f32x4v (&acc)[8][NB], bf16x8v (&fa)[4], const bf16x8v* fb, RD&& rd) {
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int n = 0; n < NB; ++n) acc[r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[r][n], 0, 0, 0);
+    if (r < RB - 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      fa[r] = rd(r);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RB - 4; ++r) {
+    __builtin_amdgcn_sched_barrier(0);
+    lgkm_wait_dyn(RB - 5 - r);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int n = 0; n < NB; ++n)
+      acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
+  }
+  __builtin_amdgcn_s_setprio(0);
+}
+
 // Epilogue of the 256-row ping-pong tiles: per row half, the wave's fp32 accumulators are
 // re-laid through its own LDS rows (64 x 68 floats), then every lane finishes 8 consecutive
 // channels of one pixel (bias, residual, ReLU or the split-bf16 forms) with 16-B accesses.
@@ -692,6 +736,32 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
+  // SEG 3 (one 32-MFMA segment per K-tile) fetches A and B of K-tile kt+2 in the R segment of kt;
+  // only with the 4-stage ring (DB = 2): the stage of kt+2 was last read in group 1's M segment
+  // of kt-2, two segments before group 0's R segment of kt
+  constexpr int SEG = (DB == 2 && ABL == 0) ? PIPNET_PP_SEG : 2;
+  if constexpr (SEG == 3) {
+    stage_a(0), stage_b(0);
+    if (1 < nk) stage_a(1), stage_b(1);
+    pp_wait_vm_dyn(1 < nk ? 4 : 0);
+    pp_barrier();
+    if (wr == 1) pp_barrier();                                 // group 1 runs one barrier behind
+    bf16x8v fa[4], fb[4];
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+      const bool pre = kt + 2 < nk;
+      if (pre) stage_a(kt + 2), stage_b(kt + 2);               // DMA before the reads (M0 write)
+      read_b(fb, st);
+      read_a(fa, st, 0);
+      if (pre) pp_wait_vm<4>();                                // A(kt+1), B(kt+1) landed
+      else pp_wait_vm<0>();
+      pp_barrier();
+      pp_mseg3<8, NB>(acc, fa, fb, [&](int r) {
+        return ds_read_b128_asm(st + (wr * 128 + 64 + r * 16) * ROWB + fofs);
+      });
+      pp_barrier();
+    }
+  } else {
   // pieces (2 per operand tile per wave) issued after B(kt + 1) by the end of phase 1 of K-tile kt:
   // A(j), B(j) for j = kt+2 .. kt+DB and A(kt+DB+1), those that exist
   auto younger_than_b = [&](int kt) {
@@ -754,6 +824,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
   int kt = 0;
   for (; kt < nk - DB - 1; ++kt) ktile(kt, IntC<1>{});
   for (; kt < nk; ++kt) ktile(kt, IntC<0>{});
+  }
   if (wr == 0) pp_barrier();                                   // re-align the groups
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   pp_barrier();                                                // stage buffers free for the epilogue
@@ -817,6 +888,7 @@ template <int EPI, int RB = 8>
 __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) {
   using namespace pp;
   constexpr int DB = 2, NS = 4;
+  constexpr int SEG = PIPNET_PPP_SEG;      // 3: A and B of K-tile kt+2 both fetched in kt's R segment
   static_assert(RB == 7 || RB == 8, "RB");
   constexpr int BMR = 32 * RB;                         // tile rows
   constexpr int NSTORE = 2 * RB;                       // epilogue 16-B stores per lane per tile
@@ -865,7 +937,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
   auto prologue_dma = [&]() {
     stage_a(0), stage_b(0);
     if (1 < nk) stage_a(1), stage_b(1);
-    if (2 < nk) stage_a(2);
+    if (SEG == 2 && 2 < nk) stage_a(2);
   };
   const int fr = lane & 15;
   const int fofs = fr * ROWB + 16 * ((lane >> 4) ^ g(fr));
@@ -879,14 +951,20 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     for (int n = 0; n < 4; ++n) fb[n] = *reinterpret_cast<const bf16x8v*>(st + BM * ROWB + (wc * 64 + n * 16) * ROWB + fofs);
   };
   // this wave's pieces issued after its B(kt + 1): A(kt+2), B(kt+2), A(kt+3), those that exist
+  // (SEG 3: A(kt+2), B(kt+2) only)
   auto younger_than_b = [&](int kt) {
-    return ((kt + 2 < nk) ? 2 + na : 0) + ((kt + 3 < nk) ? na : 0);
+    return ((kt + 2 < nk) ? 2 + na : 0) + ((SEG == 2 && kt + 3 < nk) ? na : 0);
   };
-  // the steady-state wait (2 + 2 na pieces younger than B(kt + 1)), as an immediate
+  // the steady-state wait (2 + 2 na pieces younger than B(kt + 1); SEG 3: 2 + na), as an immediate
   auto wait_steady = [&](auto extra) {
     constexpr int X = decltype(extra)::value;
-    if (RB == 8 || na == 2) pp_wait_vm<6 + X>();
-    else pp_wait_vm<4 + X>();
+    if constexpr (SEG == 3) {
+      if (RB == 8 || na == 2) pp_wait_vm<4 + X>();
+      else pp_wait_vm<3 + X>();
+    } else {
+      if (RB == 8 || na == 2) pp_wait_vm<6 + X>();
+      else pp_wait_vm<4 + X>();
+    }
   };
 
   int m0, n0;
@@ -904,6 +982,22 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
 #pragma unroll
       for (int n = 0; n < 4; ++n) acc[r][n] = f32x4v{0.f, 0.f, 0.f, 0.f};
     bf16x8v fa[4], fb[4];
+    // SEG 3: R segment (DMA of kt+2, B + half-0 A reads, counted wait) | one 32-MFMA M segment
+    auto rd1 = [&](const unsigned char* st) {
+      return [=](int r) { return ds_read_b128_asm(st + (wr * 16 * RB + 64 + r * 16) * ROWB + fofs); };
+    };
+    auto ktile3 = [&](int kt, auto steady, auto xstore) {
+      constexpr bool STEADY = decltype(steady)::value;
+      const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
+      if (STEADY || kt + 2 < nk) stage_a(kt + 2), stage_b(kt + 2);
+      read_b(fb, st);
+      read_a(fa, st, 0);
+      if constexpr (STEADY) wait_steady(xstore);
+      else pp_wait_vm_dyn(younger_than_b(kt));
+      pp_barrier();
+      pp_mseg3<RB, 4>(acc, fa, fb, rd1(st));
+      pp_barrier();
+    };
     auto ktile = [&](int kt, auto steady) {
       constexpr bool STEADY = decltype(steady)::value;
       const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
@@ -933,6 +1027,14 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
       pp_barrier();
     };
     int kt = 0;
+    if constexpr (SEG == 3) {
+      if (extra && nk > 2) {           // first K-tile after a tile switch: the previous epilogue's
+        ktile3(0, IntC<1>{}, IntC<NSTORE>{});   // stores sit between B(1) and A(2) B(2)
+        kt = 1;
+      }
+      for (; kt < nk - 2; ++kt) ktile3(kt, IntC<1>{}, IntC<0>{});
+      for (; kt < nk; ++kt) ktile3(kt, IntC<0>{}, IntC<0>{});
+    } else {
     if (extra && nk > DB + 1) {        // first K-tile after a tile switch: the stores of the
       const unsigned char* st = smem;  // previous epilogue sit between A(2) and B(2)
       stage_b(DB);
@@ -962,6 +1064,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     }
     for (; kt < nk - DB - 1; ++kt) ktile(kt, IntC<1>{});
     for (; kt < nk; ++kt) ktile(kt, IntC<0>{});
+    }
     if (wr == 0) pp_barrier();         // re-align the groups
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     pp_barrier();                      // every wave is past its last stage read
@@ -1040,7 +1143,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
     if (!more) break;
     // next tile's A(0) / B(0): younger are A1 B1 A2 (6) and this epilogue's stores (and, with a
     // residual, its loads -- already consumed, hence retired with everything older)
-    if (nk > 2) wait_steady(IntC<NSTORE>{});
+    if (nk > (SEG == 3 ? 1 : 2)) wait_steady(IntC<NSTORE>{});
     else pp_wait_vm<NSTORE>();         // fewer pieces follow B(0): wait a little longer
     pp_barrier();
     extra = 1;
@@ -1372,7 +1475,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
 
 template <int EPI, int NB = 4, int RB = 8>
 __global__ __launch_bounds__(pp::NT, 1) void conv3x3_bf16_halo_kernel(ConvParams p) {
-  conv3x3_bf16_halo_body<EPI, NB, RB, 0>(p);
+  conv3x3_bf16_halo_body<EPI, NB, RB, 0, PIPNET_HALO_SEG>(p);
 }
 
 template <int EPI, int NB, int RB, int ABL, int SEG = 2>   // tuning lab only (tools/bf16_lab.hip lab_halo)
