@@ -11,7 +11,7 @@ constexpr int DW_THREADS = 192;
 // row): C/12 lanes per pixel, each owning 3 float4 channel chunks (sl, sl + C/12, sl + C/6),
 // so one store instruction writes C/12 * 16 B contiguous of a pixel (a full 128 B line at
 // C = 96); gamma / beta stay in registers; two-pass mean / variance as torch.
-template <int C, bool S3>
+template <int C, bool S3, int ABL = 0>
 __device__ __forceinline__ void ln_rows_vec(const float* tile, int npix, int NP, int b, int H, int W, int oy0,
                                             int xblk, const float* __restrict__ lnw, const float* __restrict__ lnb,
                                             void* __restrict__ yv) {
@@ -38,23 +38,29 @@ __device__ __forceinline__ void ln_rows_vec(const float* tile, int npix, int NP,
     }
 #pragma unroll
     for (int o = LPP / 2; o > 0; o >>= 1) sm += __shfl_xor(sm, o, 64);
-    const float mean = sm * (1.0f / C);
-    float qq = 0.f;
+    float rstd = 1.0f;
+    if constexpr ((ABL & 1) == 0) {        // ABL 1 (lab): no LayerNorm statistics / shuffles
+      const float mean = sm * (1.0f / C);
+      float qq = 0.f;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      v[j] -= mean;
+      for (int j = 0; j < 3; ++j) {
+        v[j] -= mean;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) qq = fmaf(v[j][e], v[j][e], qq);
+        for (int e = 0; e < 4; ++e) qq = fmaf(v[j][e], v[j][e], qq);
+      }
+#pragma unroll
+      for (int o = LPP / 2; o > 0; o >>= 1) qq += __shfl_xor(qq, o, 64);
+      rstd = 1.0f / sqrtf(qq * (1.0f / C) + LN_EPS);
     }
-#pragma unroll
-    for (int o = LPP / 2; o > 0; o >>= 1) qq += __shfl_xor(qq, o, 64);
-    const float rstd = 1.0f / sqrtf(qq * (1.0f / C) + LN_EPS);
     if (!ok) continue;
     const int64_t opix = ((int64_t)b * H + oy) * W + ox;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const f32x4 r = v[j] * rstd * g[j] + be[j];
       const int c = 4 * (sl + LPP * j);
+      if constexpr ((ABL & 8) != 0) {       // ABL 8 (lab): no output stores (one that never fires)
+        if (!(r[0] == -1234.5f)) continue;
+      }
       if constexpr (S3) {
         __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 2 * C + c;
         __bf16 hi[4], lo[4];
@@ -76,13 +82,15 @@ __device__ __forceinline__ void ln_rows_vec(const float* tile, int npix, int NP,
 // mean / variance, coalesced NHWC stores).  1-D grid, XCD-contiguous, so the halo rows of
 // neighbouring workgroups are served from one L2.  S3: the output is written as split-bf16
 // planes [hi | lo] (2C bf16 per pixel, the A operand of the split-bf16 Linear1).
-template <int C, int TX, int TY, int MINB, bool S3 = false, int LPP = 64>
-__global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
-                                                                      const float* __restrict__ wp,
-                                                                      const float* __restrict__ bias,
-                                                                      const float* __restrict__ lnw,
-                                                                      const float* __restrict__ lnb,
-                                                                      void* __restrict__ yv) {
+// ABL (tuning lab only, tools/dw_lab.hip variants 60+; 0 in the product): 1 = no LayerNorm statistics,
+// 2 = one stencil FMA per input row instead of 7 x TX, 4 = no input loads (a lane-dependent constant),
+// 8 = no output stores, 16 = no weight loads, 32 = no LDS tile round trip (stale LDS): timing only.
+// (The body is a device function so that the product kernel's name carries no lab parameter.)
+template <int C, int TX, int TY, bool S3, int LPP, int ABL>
+__device__ __forceinline__ void dwconv7_ln_body(const float* __restrict__ x, int H, int W,
+                                                const float* __restrict__ wp, const float* __restrict__ bias,
+                                                const float* __restrict__ lnw, const float* __restrict__ lnb,
+                                                void* __restrict__ yv) {
   constexpr int QC = C / 4;
   constexpr int G = DW_THREADS / QC;
   constexpr int NP = G * TX;
@@ -121,7 +129,10 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
   for (int ir = 0; ir < TY + 6; ++ir) {
     if (ir < 7) {
 #pragma unroll
-      for (int kx = 0; kx < 7; ++kx) wrow[ir][kx] = ld4(wp + (ir * 7 + kx) * C + 4 * q);
+      for (int kx = 0; kx < 7; ++kx) {
+        if constexpr ((ABL & 16) != 0) wrow[ir][kx] = f32x4{0.5f, 0.25f, 0.125f, 1.0f} * (float)(kx + 1);
+        else wrow[ir][kx] = ld4(wp + (ir * 7 + kx) * C + 4 * q);
+      }
     }
     const int iy = oy0 + ir - 3;
     if (iy < 0 || iy >= H) continue;
@@ -129,28 +140,41 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
         (void*)(x + (((int64_t)b * H + iy) * W) * C), (short)0, W * C * 4, 0x00020000);
     f32x4 v[TX + 6];
 #pragma unroll
-    for (int r = 0; r < TX + 6; ++r)
-      v[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff0 + r * C * 4, 0, 0));
+    for (int r = 0; r < TX + 6; ++r) {
+      if constexpr ((ABL & 4) != 0) v[r] = f32x4{1.f, 2.f, 3.f, 4.f} * (float)(voff0 + r + iy);
+      else v[r] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff0 + r * C * 4, 0, 0));
+    }
 #pragma unroll
     for (int t = 0; t < TY; ++t) {
       const int ky = ir - t;
       if (ky < 0 || ky >= 7) continue;
 #pragma unroll
       for (int kx = 0; kx < 7; ++kx) {
+        if constexpr ((ABL & 2) != 0) {
+          if (kx > 0) continue;
+        }
         const f32x4 wk = wrow[ky][kx];
 #pragma unroll
         for (int px = 0; px < TX; ++px) acc[t][px] += v[px + kx] * wk;
       }
+      if constexpr ((ABL & 2) != 0) {                  // keep every loaded column live
+#pragma unroll
+        for (int px = 0; px < TX; ++px) acc[t][px] += v[px + 6];
+      }
     }
   }
+  if constexpr ((ABL & 32) == 0) {
 #pragma unroll
-  for (int t = 0; t < TY; ++t)
+    for (int t = 0; t < TY; ++t)
 #pragma unroll
-    for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
-  __syncthreads();
+      for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
+    __syncthreads();
+  } else {
+    if (acc[0][0][0] == -1234.5f) tile[tid] = 0.f;     // keep the stencil live; no round trip
+  }
 
   if constexpr (LPP * 12 == C) {
-    ln_rows_vec<C, S3>(tile, TY * NP, NP, b, H, W, oy0, xblk, lnw, lnb, yv);
+    ln_rows_vec<C, S3, ABL>(tile, TY * NP, NP, b, H, W, oy0, xblk, lnw, lnb, yv);
     return;
   }
   // LayerNorm: LPP lanes per pixel (64 / LPP pixels per wave at once, log2(LPP)-step
@@ -209,6 +233,36 @@ __global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const floa
       }
     }
   }
+}
+
+template <int C, int TX, int TY, int MINB, bool S3 = false, int LPP = 64>
+__global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_kernel(const float* __restrict__ x, int H, int W,
+                                                                      const float* __restrict__ wp,
+                                                                      const float* __restrict__ bias,
+                                                                      const float* __restrict__ lnw,
+                                                                      const float* __restrict__ lnb,
+                                                                      void* __restrict__ yv) {
+  dwconv7_ln_body<C, TX, TY, S3, LPP, 0>(x, H, W, wp, bias, lnw, lnb, yv);
+}
+
+template <int C, int TX, int TY, int MINB, int LPP, int ABL>   // tuning lab only (tools/dw_lab.hip)
+__global__ __launch_bounds__(DW_THREADS, MINB) void dwconv7_ln_abl_kernel(const float* __restrict__ x, int H, int W,
+                                                                          const float* __restrict__ wp,
+                                                                          const float* __restrict__ bias,
+                                                                          const float* __restrict__ lnw,
+                                                                          const float* __restrict__ lnb,
+                                                                          void* __restrict__ yv) {
+  dwconv7_ln_body<C, TX, TY, false, LPP, ABL>(x, H, W, wp, bias, lnw, lnb, yv);
+}
+
+template <int C, int TX, int TY, int MINB, int LPP, int ABL>
+inline int launch_dw_abl(const float* x, int B, int H, int W, const float* wp, const float* bias, const float* lnw,
+                         const float* lnb, void* y, hipStream_t s) {
+  constexpr int NP = (DW_THREADS / (C / 4)) * TX;
+  const dim3 grid(((W + NP - 1) / NP) * ((H + TY - 1) / TY) * B);
+  hipLaunchKernelGGL((dwconv7_ln_abl_kernel<C, TX, TY, MINB, LPP, ABL>), grid, dim3(DW_THREADS), 0, s, x, H, W, wp,
+                     bias, lnw, lnb, y);
+  return hipGetLastError() == hipSuccess ? PIPNET_OK : PIPNET_ERR_LAUNCH;
 }
 
 template <int C, int TX, int TY, int MINB, bool S3 = false, int LPP = 64>

@@ -59,6 +59,16 @@ extern "C" int lab_dw(int variant, const float* x, int B, int H, int W, int C, c
   A(11, 384, 4, 1, 2, 32, 1) A(12, 384, 4, 1, 2, 32, 2) A(14, 384, 4, 1, 2, 32, 4) A(13, 384, 4, 1, 2, 32, 3)
   A(16, 384, 4, 1, 2, 32, 6)
 #undef A
+  // v60-v69 (round 6): ablations of the PRODUCT kernels (dwconv7_ln_abl_kernel = the product body with
+  // ABL bits: 1 no LN statistics, 2 one FMA per row, 4 no input loads, 8 no stores, 16 no weight
+  // loads, 32 no LDS tile round trip) at the product's tiles: 384 -> (7, 3), 768 -> (13, 1), 96 -> (7, 2)
+#define PA(ID, ABL)                                                                                                 \
+  if (variant == ID && C == 384) return launch_dw_abl<384, 7, 3, 1, 32, ABL>(x, B, H, W, wp, bias, lnw, lnb, y, s); \
+  if (variant == ID && C == 768) return launch_dw_abl<768, 13, 1, 1, 64, ABL>(x, B, H, W, wp, bias, lnw, lnb, y, s); \
+  if (variant == ID && C == 96) return launch_dw_abl<96, 7, 2, 1, 8, ABL>(x, B, H, W, wp, bias, lnw, lnb, y, s);
+  PA(60, 0) PA(61, 1) PA(62, 2) PA(63, 4) PA(64, 8) PA(65, 16) PA(66, 32) PA(67, 33) PA(68, 6) PA(69, 22)
+  PA(70, 41) PA(71, 9) PA(72, 54) PA(73, 20)
+#undef PA
 #undef V
 #undef R
   return 1;

@@ -80,3 +80,39 @@ if "--abl" in sys.argv:
             out.append(f"v{v}:{min(ts):6.1f}us")
         print(f"ablation C={c} ({'full', 'noLN', 'noFMA', 'noLoad', 'noLN+noFMA', 'noFMA+noLoad'}): " + " ".join(out),
               flush=True)
+
+# round 6: ablation of the PRODUCT kernel bodies (v60 = product, checked bitwise against the library's
+# pipnet_dwconv7_ln_f32) at C2's stage-3 / stage-4 / stage-1 shapes, batch 64
+if "--abl6" in sys.argv:
+    from count_pipnet_amd import kernels as K
+    names = {60: "product", 61: "noLNstats", 62: "1FMA/row", 63: "noLoads", 64: "noStores", 65: "noWeights",
+             66: "noLDStile", 67: "noLDS+noLN", 68: "noFMA+noLoads", 69: "noW+noLd+noFMA", 70: "noLDS+noSt+noLN",
+             71: "noLN+noSt", 72: "LN+stores only", 73: "noLoads+noW"}
+    for c, hw in [(384, 27), (768, 26), (96, 56)]:
+        g = torch.Generator(device=dev).manual_seed(c)
+        x = torch.randn(64, hw, hw, c, device=dev, generator=g)
+        w = torch.randn(49, c, device=dev, generator=g) * 0.2
+        b, lw, lb = (torch.randn(c, device=dev, generator=g) for _ in range(3))
+        y = torch.empty_like(x)
+        ref = K.dwconv7_ln(x, w, b, lw, lb)
+        assert lib.lab_dw(60, x.data_ptr(), 64, hw, hw, c, w.data_ptr(), b.data_ptr(), lw.data_ptr(), lb.data_ptr(),
+                          y.data_ptr(), stream, 2048, 7) == 0
+        torch.cuda.synchronize()
+        same = torch.equal(y, ref)
+        gb = 2 * x.numel() * 4 / 1e9
+        ts = {v: [] for v in names}
+        for _ in range(3):
+            for v in names:
+                args = (v, x.data_ptr(), 64, hw, hw, c, w.data_ptr(), b.data_ptr(), lw.data_ptr(), lb.data_ptr(),
+                        y.data_ptr(), stream, 2048, 7)
+                assert lib.lab_dw(*args) == 0, v
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    lib.lab_dw(*args)
+                e1.record()
+                torch.cuda.synchronize()
+                ts[v].append(e0.elapsed_time(e1) / 10 * 1e3)
+        med = {v: sorted(t)[1] for v, t in ts.items()}
+        print(f"C={c} H=W={hw} batch 64 ({gb * 1e3:.0f} MB algorithmic; v60 bitwise the library: {same}): " +
+              "  ".join(f"{names[v]} {med[v]:.1f}us/{gb / med[v] * 1e6 / 1e3:.2f}TB/s" for v in names), flush=True)
