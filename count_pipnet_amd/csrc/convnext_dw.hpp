@@ -59,7 +59,7 @@ __device__ __forceinline__ void ln_rows_vec(const float* tile, int npix, int NP,
       const f32x4 r = v[j] * rstd * g[j] + be[j];
       const int c = 4 * (sl + LPP * j);
       if constexpr ((ABL & 8) != 0) {       // ABL 8 (lab): no output stores (one that never fires)
-        if (!(r[0] == -1234.5f)) continue;
+        if (!(r[0] + r[1] + r[2] + r[3] == -1234.5f)) continue;
       }
       if constexpr (S3) {
         __bf16* dst = reinterpret_cast<__bf16*>(yv) + opix * 2 * C + c;
@@ -169,8 +169,13 @@ __device__ __forceinline__ void dwconv7_ln_body(const float* __restrict__ x, int
 #pragma unroll
       for (int i = 0; i < TX; ++i) st4(tile + (t * NP + g * TX + i) * C + 4 * q, acc[t][i]);
     __syncthreads();
-  } else {
-    if (acc[0][0][0] == -1234.5f) tile[tid] = 0.f;     // keep the stencil live; no round trip
+  } else {                                           // keep every accumulator live; no round trip
+    f32x4 keep = acc[0][0];
+#pragma unroll
+    for (int t = 0; t < TY; ++t)
+#pragma unroll
+      for (int i = 0; i < TX; ++i) keep += acc[t][i];
+    if (keep[0] + keep[1] + keep[2] + keep[3] == -1234.5f) tile[tid] = 0.f;
   }
 
   if constexpr (LPP * 12 == C) {

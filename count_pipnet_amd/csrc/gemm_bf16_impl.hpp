@@ -1348,6 +1348,11 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          // zero block written
   pp_barrier();
   if (wr == 1) pp_barrier();                                   // group 1 runs one barrier behind
+  // lab ABL 64: static priority for the younger half (waves 4-7) instead of per-segment flips
+  // (cdna_hip_programming.md T5 static form); ABL 128: no s_setprio at all
+  if constexpr ((ABL & 64) != 0) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
 
   // K-tile kt = 18 P + 2 t + h.  B of K-tile kt+2 is fetched in phase 0 of kt; the halo of
   // pair P+1 in phase 1 of (t, h) = (0, 1).  The wait in phase 1 of kt retires B(kt+1): younger
@@ -1394,7 +1399,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
           else pp_wait_vm<L::BPW>();
           hbar();
           // ---- M segment: 16 MFMAs of half 0 with half 1's A reads interleaved, 16 of half 1 ----
-          __builtin_amdgcn_s_setprio(1);
+          if constexpr ((ABL & (64 | 128)) == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -1421,7 +1426,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
             for (int n = 0; n < NB; ++n)
               acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
           }
-          __builtin_amdgcn_s_setprio(0);
+          if constexpr ((ABL & (64 | 128)) == 0) __builtin_amdgcn_s_setprio(0);
           hbar();
           continue;
         }

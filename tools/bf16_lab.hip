@@ -758,7 +758,7 @@ extern "C" int lab_halo(int abl, const void* x, int B, int H, int W, int Cin, co
     HALO_CASE(19) HALO_CASE(10) HALO_CASE(12) HALO_CASE(27)
     HALO1_CASE(0) HALO1_CASE(1) HALO1_CASE(2) HALO1_CASE(4) HALO1_CASE(8) HALO1_CASE(16) HALO1_CASE(3)
     HALO1_CASE(17) HALO1_CASE(19) HALO1_CASE(27)
-    HALO3_CASE(0) HALO3_CASE(2) HALO3_CASE(19) HALO3_CASE(3)
+    HALO3_CASE(0) HALO3_CASE(2) HALO3_CASE(19) HALO3_CASE(3) HALO3_CASE(64) HALO3_CASE(128) HALO3_CASE(83)
     default: return 1;
   }
 #undef HALO_CASE

@@ -3,5 +3,5 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out
-HALO_VARIANTS=${HALO_VARIANTS:-0,1000,3000,2,1002,3002,19,1019,3019} timeout -k 10 300 python3 tools/halo_lab.py > gpurun_out/halo_lab.txt 2>&1
+HALO_VARIANTS=${HALO_VARIANTS:-0,3000,3064,3128,3019,3083} timeout -k 10 300 python3 tools/halo_lab.py > gpurun_out/halo_lab.txt 2>&1
 rc=$?; cat gpurun_out/halo_lab.txt; exit $rc
