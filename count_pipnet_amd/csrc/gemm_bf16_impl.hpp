@@ -526,6 +526,22 @@ PIPNET_DEV void lgkm_wait_dyn(int n) {        // n compile-time after unrolling
 #ifndef PIPNET_PPP_SEG
 #define PIPNET_PPP_SEG 3
 #endif
+// Matrix-segment priority of the SEG 3 schedules: 1 = s_setprio 1 around every M segment (the
+// product), 0 = none, 2 = one static s_setprio 1 for the younger half (waves 4-7) before the loop
+#ifndef PIPNET_BF16_PRIO
+#define PIPNET_BF16_PRIO 1
+#endif
+PIPNET_DEV void seg_prio(int on) {
+  if constexpr (PIPNET_BF16_PRIO == 1) {
+    if (on) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
+PIPNET_DEV void static_prio() {
+  if constexpr (PIPNET_BF16_PRIO == 2) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+  }
+}
 
 // The SEG = 3 M segment: half 0's 4 x NB MFMAs, each row followed by the untracked read of the
 // half-1 fragment that reuses its registers, then half 1's (RB - 4) x NB MFMAs, each row after a
@@ -533,7 +549,7 @@ PIPNET_DEV void lgkm_wait_dyn(int n) {        // n compile-time after unrolling
 // ds_read_b128_asm.
 template <int RB, int NB, typename RD>
 PIPNET_DEV void pp_mseg3(f32x4v (&acc)[8][NB], bf16x8v (&fa)[4], const bf16x8v* fb, RD&& rd) {
-  __builtin_amdgcn_s_setprio(1);
+  seg_prio(1);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -553,7 +569,7 @@ PIPNET_DEV void pp_mseg3(f32x4v (&acc)[8][NB], bf16x8v (&fa)[4], const bf16x8v* 
     for (int n = 0; n < NB; ++n)
       acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
   }
-  __builtin_amdgcn_s_setprio(0);
+  seg_prio(0);
 }
 
 // Epilogue of the 256-row ping-pong tiles: per row half, the wave's fp32 accumulators are
@@ -746,6 +762,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_pp_kernel(ConvParams p) {
     pp_wait_vm_dyn(1 < nk ? 4 : 0);
     pp_barrier();
     if (wr == 1) pp_barrier();                                 // group 1 runs one barrier behind
+    static_prio();
     bf16x8v fa[4], fb[4];
     for (int kt = 0; kt < nk; ++kt) {
       const unsigned char* st = smem + (kt % NS) * STAGE_BYTES;
@@ -974,6 +991,7 @@ __global__ __launch_bounds__(pp::NT, 1) void conv_bf16_ppp_kernel(ConvParams p) 
   pp_wait_vm_dyn(younger_than_b(-1));
   pp_barrier();
   int extra = 0;                       // epilogue stores younger than this tile's first B(1)
+  if constexpr (SEG == 3) static_prio();
   for (;;) {
     if (wr == 1) pp_barrier();         // group 1 runs one barrier behind
     f32x4v acc[8][4];
@@ -1353,6 +1371,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
   if constexpr ((ABL & 64) != 0) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
   }
+  if constexpr (SEG == 3 && ABL == 0) static_prio();
 
   // K-tile kt = 18 P + 2 t + h.  B of K-tile kt+2 is fetched in phase 0 of kt; the halo of
   // pair P+1 in phase 1 of (t, h) = (0, 1).  The wait in phase 1 of kt retires B(kt+1): younger
@@ -1399,7 +1418,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
           else pp_wait_vm<L::BPW>();
           hbar();
           // ---- M segment: 16 MFMAs of half 0 with half 1's A reads interleaved, 16 of half 1 ----
-          if constexpr ((ABL & (64 | 128)) == 0) __builtin_amdgcn_s_setprio(1);
+          if constexpr ((ABL & (64 | 128)) == 0) seg_prio(1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -1426,7 +1445,7 @@ __device__ __forceinline__ void conv3x3_bf16_halo_body(const ConvParams& p) {
             for (int n = 0; n < NB; ++n)
               acc[4 + r][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[r], fb[n], acc[4 + r][n], 0, 0, 0);
           }
-          if constexpr ((ABL & (64 | 128)) == 0) __builtin_amdgcn_s_setprio(0);
+          if constexpr ((ABL & (64 | 128)) == 0) seg_prio(0);
           hbar();
           continue;
         }
