@@ -23,7 +23,8 @@ int choose_group_m(const GemmParams& p) {
 //   or M <= 64
 //   otherwise                 BK=32, 128-row tiles, 2 LDS stages      (stage-3/4 fc1, fc2)
 // 0 = register-staged K-tail kernel, 1 = BK16x128 rows x3 stages, 2 = BK32x64 rows,
-// 3 = BK32x128 rows (mirrored by count_pipnet_amd/kernels.py:gemm_kernel_name)
+// 3 = BK32x128 rows, 4 = BK32x256 rows on 8 waves (exported by pipnet_linear_f32_plan; the
+// profiling labels of count_pipnet_amd/kernels.py:gemm_kernel_name come from it)
 // (PIPNET_AB_GEMM_RULE: build-time A/B hook for tools/ab_build.py, 0 in the product)
 #ifndef PIPNET_AB_GEMM_RULE
 #define PIPNET_AB_GEMM_RULE 0
@@ -39,6 +40,12 @@ int gemm_variant(int M, int N, int K, bool vec) {
   // four interleaved rounds (profiles/r05/ab_c5_addon_tile.txt).  Same K order: bitwise equal.
   if (N >= 1024 && N % BN == 0 && K <= 192 && M > 64) return 3;
   if (N <= 384 || K <= 192 || M <= 64) return 2;
+  // long-K (>= 768) 128-row-tile GEMMs with a full round of 256-row tiles: the 8-wave 256 x 128
+  // workgroup (4 x 2 waves of the same 64 x 64 wave tile, the same K order: bitwise the 4-wave
+  // tile), one per CU -- the B panel is shared by twice the rows and a CU's LDS-DMA stream is one
+  // workgroup's: stage-4 fc1 / fc2 +4..8 % (round 6, profiles/r06/gemm_tn8_lab.txt).  A per-shape
+  // rule like the others (the arithmetic of a row never depends on it).
+  if (PIPNET_AB_GEMM_RULE != 3 && K >= 768 && N % BN == 0 && (int64_t)((M + 255) / 256) * (N / BN) >= 256) return 4;
   return 3;
 }
 
@@ -100,11 +107,13 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
   const int v = gemm_variant(p.M, p.N, p.K, vec);
-  p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
-  const dim3 grid(p.mt * p.nt), block(NTHREADS);
+  const int bm = v == 2 ? 64 : (v == 4 ? 256 : 128);
+  p.mt = (p.M + bm - 1) / bm;
+  const dim3 grid(p.mt * p.nt), block(v == 4 ? 512 : NTHREADS);
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
-    if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
+    if (v == 4) hipLaunchKernelGGL((gemm_f32_tn8_kernel<32, 2, E, ALOAD, 1, 2>), grid, block, 0, s, p);   \
+    else if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p); \
     else if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2, 0, true>), grid, \
                                                    block, 0, s, p);                                         \
     else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2>), grid, block, 0, s, p); \
@@ -129,6 +138,13 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
 }
 
 }  // namespace
+
+// The variant pipnet_linear_f32 / _rowscale / pipnet_conv2x2_f32 / pipnet_conv2d_nhwc_f32 launch for an
+// M x N x K product with dense, unit-stride, 16-B aligned operands (what torch allocations give).
+extern "C" int pipnet_linear_f32_plan(int M, int N, int K) {
+  if (M < 0 || N < 0 || K <= 0) return -PIPNET_ERR_ARG;
+  return gemm_variant(M, N, K, true);
+}
 
 extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,
                                  const float* scale, const float* R, int64_t ldr, float* C, int64_t ldc,

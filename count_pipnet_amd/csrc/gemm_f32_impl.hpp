@@ -437,13 +437,16 @@ PIPNET_DEV void zero_acc(Acc& acc) {
 // ======================================================================================
 // main path: LDS-DMA staging, swizzled rows, pipelined fragments (K % BK == 0)
 // ======================================================================================
-template <int BK, int TM>
+// WGM = waves along M (2: the 4-wave 2x2 workgroup; 4: the 8-wave 4x2 workgroup of the long-K
+// stage-4 GEMMs, gemm_f32.hip variant 4 -- same wave tile, same K order, bitwise the 4-wave rows)
+template <int BK, int TM, int WGM = 2>
 struct Geo {
-  static constexpr int BMT = 64 * TM;                     // tile rows of A
+  static constexpr int NW = 2 * WGM;                      // waves per workgroup
+  static constexpr int BMT = 32 * TM * WGM;               // tile rows of A
   static constexpr int CHUNKS = BK / 4;                   // 16-B chunks per LDS row
   static constexpr int ROWS_PER_DMA = 64 / CHUNKS;        // rows one 1-KiB DMA fills
-  static constexpr int A_DMA = BMT / ROWS_PER_DMA / NWAVES;
-  static constexpr int B_DMA = BN / ROWS_PER_DMA / NWAVES;
+  static constexpr int A_DMA = BMT / ROWS_PER_DMA / NW;
+  static constexpr int B_DMA = BN / ROWS_PER_DMA / NW;
   static constexpr int TILE_FLOATS = (BMT + BN) * BK;     // one buffer: A rows then B rows
   static constexpr int NGROUPS = BK / 8;                  // 4-deep fragment groups per half-wave
   // chunk swizzle: the 16 lanes of a ds_read_b128 group read 16 distinct bank slots
@@ -456,9 +459,9 @@ struct Frag {
   f32x4 a[2], b[2];
 };
 
-template <int BK, int TM>
+template <int BK, int TM, int WGM = 2>
 PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int lh, int q) {
-  using G = Geo<BK, TM>;
+  using G = Geo<BK, TM, WGM>;
   const int c = lh * (G::CHUNKS / 2) + q;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -495,9 +498,9 @@ struct Frag16 {
   f32x4 a[4], b[4];
 };
 
-template <int BK, int TM>
+template <int BK, int TM, int WGM = 2>
 PIPNET_DEV void read_frag16(Frag16& f, const float* buf, int wm, int wn, int lane, int q) {
-  using G = Geo<BK, TM>;
+  using G = Geo<BK, TM, WGM>;
   const int r16 = lane & 15, c = 4 * q + (lane >> 4);
 #pragma unroll
   for (int ib = 0; ib < 2 * TM; ++ib) {
@@ -549,9 +552,10 @@ PIPNET_DEV void wait_dma_barrier() {
 // workgroups land on different SIMDs (a relabelling: every output is computed identically).
 // SH = MFMA shape: 0 = v_mfma_f32_32x32x2_f32, 1 = v_mfma_f32_16x16x4_f32 (same tile, LDS image,
 // DMA and fragment bytes; a different k order inside each K-tile, so a different rounding).
-template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD>
+template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD, int WGM = 2>
 PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
-  using G = Geo<BK, TM>;
+  using G = Geo<BK, TM, WGM>;
+  constexpr int NWAVES = G::NW;
   static_assert(SH == 0 || BK == 32, "16x16x4 fragments: BK 32 (the swizzle is conflict-free there)");
   // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
   const int nk_all = p.K / BK;
@@ -559,7 +563,7 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
   const int nk = (int)((int64_t)nk_all * (blockIdx.y + 1) / gridDim.y) - kt_begin;
   p.C += (int64_t)blockIdx.y * p.split_stride;
   constexpr int DMA_PER_TILE = G::A_DMA + G::B_DMA;     // per wave
-  static_assert(NS * G::TILE_FLOATS >= 4 * 32 * 64, "vector epilogue needs 32 KiB of LDS");
+  static_assert(NS * G::TILE_FLOATS >= NWAVES * 32 * 64, "vector epilogue needs 8 KiB of LDS per wave");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -655,7 +659,7 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
     if constexpr (SH == 1) {
       // 2 fragment groups of 64 MFMAs (2048 cycles per wave) per 32-deep K-tile
       Frag16 fa, fb;
-      read_frag16<BK, TM>(fa, smem, wm, wn, lane, 0);
+      read_frag16<BK, TM, WGM>(fa, smem, wm, wn, lane, 0);
       int cur = 0;
       for (int kt = 0; kt < nk; ++kt) {
         const float* buf = smem + cur * G::TILE_FLOATS;
@@ -665,18 +669,18 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
           stage(kt + NS - 1, nb);
           issued = kt + NS - 1;
         }
-        read_frag16<BK, TM>(fb, buf, wm, wn, lane, 1);
+        read_frag16<BK, TM, WGM>(fb, buf, wm, wn, lane, 1);
         mfma_frag16<TM, JL>(acc, fa);
         const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
         if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);
-        if (kt + 1 < nk) read_frag16<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lane, 0);
+        if (kt + 1 < nk) read_frag16<BK, TM, WGM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lane, 0);
         mfma_frag16<TM, JL>(acc, fb);
         cur = nxt;
       }
       return;
     } else {
     Frag fa, fb;
-    read_frag<BK, TM>(fa, smem, wm, wn, lr, lh, 0);
+    read_frag<BK, TM, WGM>(fa, smem, wm, wn, lr, lh, 0);
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const float* buf = smem + cur * G::TILE_FLOATS;
@@ -687,19 +691,19 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
         issued = kt + NS - 1;
       }
       if constexpr (G::NGROUPS == 4) {
-        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 1);
         mfma_frag<TM, JL>(acc, fa);
-        read_frag<BK, TM>(fa, buf, wm, wn, lr, lh, 2);
+        read_frag<BK, TM, WGM>(fa, buf, wm, wn, lr, lh, 2);
         mfma_frag<TM, JL>(acc, fb);
-        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 3);
+        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 3);
         mfma_frag<TM, JL>(acc, fa);
       } else {
-        read_frag<BK, TM>(fb, buf, wm, wn, lr, lh, 1);
+        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 1);
         mfma_frag<TM, JL>(acc, fa);
       }
       const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
       if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
-      if (kt + 1 < nk) read_frag<BK, TM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
+      if (kt + 1 < nk) read_frag<BK, TM, WGM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
       mfma_frag<TM, JL>(acc, fb);
       cur = nxt;
     }
@@ -718,7 +722,7 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
     float t = 0.f;
 #pragma unroll
     for (int v = 0; v < 64; ++v) t += av[v];
-    p.C[(int64_t)blockIdx.x * NTHREADS + tid] = t;
+    p.C[(int64_t)blockIdx.x * 64 * NWAVES + tid] = t;
     return;
   }
   if (p.vec_epi)
@@ -737,6 +741,14 @@ template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS = 2, int ABL = 0,
 __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM>::TILE_FLOATS];
   gemm_tn_body<0, BK, TM, EPI, ALOAD, NS, ABL, NPAD>(p, smem);
+}
+
+// 8-wave form (WGM = 4): a (128 TM) x 128 tile, waves 4 (M) x 2 (N) of the same (32 TM) x 64 wave
+// tile (product variant 4; tuning lab tools/gemm_lab.hip variants 60+)
+template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS, int ABL = 0, int SH = 0>
+__global__ __launch_bounds__(512, MINB) void gemm_f32_tn8_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM, 4>::TILE_FLOATS];
+  gemm_tn_body<SH, BK, TM, EPI, ALOAD, NS, ABL, false, 4>(p, smem);
 }
 
 // the same tile on v_mfma_f32_16x16x4_f32

@@ -36,20 +36,30 @@ def _launch(kname: str, flops: float, fn) -> None:
         _launch_hook(kname, flops, fn)
 
 
+@functools.lru_cache(maxsize=4096)
+def gemm_variant(m: int, n: int, k: int) -> int:
+    """The fp32 GEMM variant the library launches for an m x n x k product (pipnet_linear_f32_plan:
+    the library's own rule, csrc/gemm_f32.hip gemm_variant -- never mirrored here)."""
+    v = _lib.load().pipnet_linear_f32_plan(m, n, k)
+    if v < 0:
+        raise RuntimeError(f"linear: no GEMM variant for {m} x {n} x {k}")
+    return v
+
+
 def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
-    """The rocprof name of the GEMM instantiation the library picks (mirrors gemm_variant and
-    launch_gemm in csrc/gemm_f32.hip for dense, unit-stride operands: leading dimensions equal
-    to K / N, 16-B aligned torch allocations -- so ``vec_epi`` holds whenever N % 4 == 0)."""
-    if k % 16 == 0 and ((k <= 96 and n > 192 and m > 64) or (k % 32 and m > 64)):
+    """The rocprof name of the GEMM instantiation the library picks (dense, unit-stride, 16-B
+    aligned torch operands -- so ``vec_epi`` holds whenever N % 4 == 0)."""
+    v = gemm_variant(m, n, k)
+    if v == 1:
         return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
-    if k % 32:
+    if v == 0:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
-    if n >= 1024 and n % 128 == 0 and k <= 192 and m > 64:
+    if v == 4:
+        return f"pipnet_gemm::gemm_f32_tn8_kernel<32, 2, {epilogue}, {aload}, 1, 2, 0, 0>"
+    if v == 3:
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
-    if n <= 384 or k <= 192 or m <= 64:
-        npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
-        return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
-    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
+    npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped
+    return f"pipnet_gemm::gemm_f32_tn_kernel<32, 1, {epilogue}, {aload}, 3, 2, 0, {npad}>"
 
 
 _CUS = {}

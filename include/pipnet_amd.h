@@ -53,7 +53,8 @@ extern "C" {
  * pipnet_linear_agelu_f32 are gone -- kernel selection is a fixed per-shape rule with no
  * mutable library state -- and the one-launch fused head pipnet_softmax_pool_linear_f32 / _bf16
  * (+ _part_floats) and pipnet_matmul2_f64acc_f32 are new (round 5).  A caller built against an older version must not bind this library.
- * Round 6 only ADDS entry points (pipnet_philox_exp1_f32, pipnet_conv2d_nhwc_bf16_plan); no signature changed. */
+ * Round 6 only ADDS entry points (pipnet_philox_exp1_f32, pipnet_conv2d_nhwc_bf16_plan,
+ * pipnet_linear_f32_plan); no signature changed. */
 #define PIPNET_AMD_ABI_VERSION 3
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -338,6 +339,11 @@ int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int HW, int P, f
  * form); log_e = 1: log E on the hard head's hardware-log form.  Replaces the
  * `-torch.empty_like(x).exponential_().log()` draw inside F.gumbel_softmax (count_pipnet_utils.py:36-38). */
 int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e, float* out, void* stream);
+
+/* fp32 GEMM variant plan: the variant pipnet_linear_f32 (and the conv / rowscale forms) launch for an
+ * M x N x K product with dense 16-B aligned operands -- 0 K-tail kernel, 1 BK16 128-row, 2 BK32
+ * 64-row, 3 BK32 128-row, 4 BK32 256-row on 8 waves -- or -PIPNET_ERR_ARG (profiling labels). */
+int pipnet_linear_f32_plan(int M, int N, int K);
 
 /* bf16 conv tile plan: the tile id pipnet_conv2d_nhwc_bf16_tile takes for this shape / epilogue
  * (tile -1 = the automatic choice, >= 0 validated), or -PIPNET_ERR_ARG.  The library's own rule,

@@ -39,6 +39,21 @@ static void launch(GemmParams& p, int epi, hipStream_t s) {
     hipLaunchKernelGGL((gemm_f32_tn_kernel<BK, TM, PIPNET_EPI_NONE, ALOAD_DENSE, MINB, NS, ABL>), grid, block, 0, s, p);
 }
 
+// round 6: the 8-wave workgroup (WGM = 4): (128 TM) x 128 tiles, one workgroup per CU
+template <int BK, int TM, int MINB, int NS, int ABL = 0, int SH = 0>
+static void launch8(GemmParams& p, int epi, hipStream_t s) {
+  p.mt = (p.M + 128 * TM - 1) / (128 * TM);
+  const dim3 grid(p.mt * p.nt), block(512);
+  if (epi == PIPNET_EPI_BIAS_GELU)
+    hipLaunchKernelGGL((gemm_f32_tn8_kernel<BK, TM, PIPNET_EPI_BIAS_GELU, ALOAD_DENSE, MINB, NS, ABL, SH>), grid, block, 0, s, p);
+  else if (epi == PIPNET_EPI_BIAS)
+    hipLaunchKernelGGL((gemm_f32_tn8_kernel<BK, TM, PIPNET_EPI_BIAS, ALOAD_DENSE, MINB, NS, ABL, SH>), grid, block, 0, s, p);
+  else if (epi == PIPNET_EPI_RESID)
+    hipLaunchKernelGGL((gemm_f32_tn8_kernel<BK, TM, PIPNET_EPI_RESID, ALOAD_DENSE, MINB, NS, ABL, SH>), grid, block, 0, s, p);
+  else
+    hipLaunchKernelGGL((gemm_f32_tn8_kernel<BK, TM, PIPNET_EPI_NONE, ALOAD_DENSE, MINB, NS, ABL, SH>), grid, block, 0, s, p);
+}
+
 static long long* g_stamps = nullptr;
 extern "C" void lab_set_stamps(long long* p) { g_stamps = p; }
 
@@ -70,6 +85,12 @@ extern "C" int lab_linear(int variant, int group_m, const float* A, int64_t lda,
     case 6: launch<16, 1, 3, 4>(p, epi, s); break;
     case 7: launch<16, 2, 3, 3>(p, epi, s); break;    // 48 KiB LDS, <=168 VGPRs: 3 workgroups / CU
     case 8: launch<16, 2, 3, 2>(p, epi, s); break;    // 32 KiB LDS, 3 workgroups / CU
+    // round 6: 8-wave workgroups -- 60/61: 256 x 128 tiles with 3 / 2 LDS stages; 62/63: 128 x 128 with 4 / 3
+    case 60: launch8<32, 2, 1, 3>(p, epi, s); break;
+    case 61: launch8<32, 2, 1, 2>(p, epi, s); break;
+    case 62: launch8<32, 1, 1, 4>(p, epi, s); break;
+    case 63: launch8<32, 1, 1, 3>(p, epi, s); break;
+    case 64: launch8<32, 2, 1, 3, 0, 1>(p, epi, s); break;      // 60 on v_mfma_f32_16x16x4_f32
     // ablations of variant 0 (timing only; outputs are wrong)
     case 10: launch<32, 2, 2, 2, 1>(p, epi, s); break;
     case 11: launch<32, 2, 2, 2, 2>(p, epi, s); break;

@@ -63,7 +63,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 times.setdefault((v, gm, epi), []).append(e0.elapsed_time(e1) / 5 * 1e-3)
-                if rnd == 0 and (v < 10 or 40 <= v < 60):
+                if rnd == 0 and (v < 10 or 40 <= v < 70):
                     if epi not in ref:
                         ref[epi] = C.clone()
                     else:
