@@ -23,8 +23,10 @@ int choose_group_m(const GemmParams& p) {
 //   or M <= 64
 //   otherwise                 BK=32, 128-row tiles, 2 LDS stages      (stage-3/4 fc1, fc2)
 // 0 = register-staged K-tail kernel, 1 = BK16x128 rows x3 stages, 2 = BK32x64 rows,
-// 3 = BK32x128 rows, 4 = BK32x256 rows on 8 waves (exported by pipnet_linear_f32_plan; the
-// profiling labels of count_pipnet_amd/kernels.py:gemm_kernel_name come from it)
+// 3 = BK32x128 rows (exported by pipnet_linear_f32_plan; the profiling labels of
+// count_pipnet_amd/kernels.py:gemm_kernel_name come from it).  An 8-wave 256 x 128 workgroup
+// (gemm_f32_impl.hpp gemm_f32_tn8_kernel, tools/gemm_lab.hip 60+) beat variant 3 by 4-8 % on the
+// stage-4 shapes in the lab but not inside C2 (profiles/r06/gemm_tn8_ab.txt): not dispatched.
 // (PIPNET_AB_GEMM_RULE: build-time A/B hook for tools/ab_build.py, 0 in the product)
 #ifndef PIPNET_AB_GEMM_RULE
 #define PIPNET_AB_GEMM_RULE 0
@@ -40,12 +42,6 @@ int gemm_variant(int M, int N, int K, bool vec) {
   // four interleaved rounds (profiles/r05/ab_c5_addon_tile.txt).  Same K order: bitwise equal.
   if (N >= 1024 && N % BN == 0 && K <= 192 && M > 64) return 3;
   if (N <= 384 || K <= 192 || M <= 64) return 2;
-  // long-K (>= 768) 128-row-tile GEMMs with a full round of 256-row tiles: the 8-wave 256 x 128
-  // workgroup (4 x 2 waves of the same 64 x 64 wave tile, the same K order: bitwise the 4-wave
-  // tile), one per CU -- the B panel is shared by twice the rows and a CU's LDS-DMA stream is one
-  // workgroup's: stage-4 fc1 / fc2 +4..8 % (round 6, profiles/r06/gemm_tn8_lab.txt).  A per-shape
-  // rule like the others (the arithmetic of a row never depends on it).
-  if (PIPNET_AB_GEMM_RULE != 3 && K >= 768 && N % BN == 0 && (int64_t)((M + 255) / 256) * (N / BN) >= 256) return 4;
   return 3;
 }
 
@@ -107,13 +103,11 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
   const int v = gemm_variant(p.M, p.N, p.K, vec);
-  const int bm = v == 2 ? 64 : (v == 4 ? 256 : 128);
-  p.mt = (p.M + bm - 1) / bm;
-  const dim3 grid(p.mt * p.nt), block(v == 4 ? 512 : NTHREADS);
+  p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
+  const dim3 grid(p.mt * p.nt), block(NTHREADS);
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
-    if (v == 4) hipLaunchKernelGGL((gemm_f32_tn8_kernel<32, 2, E, ALOAD, 1, 2>), grid, block, 0, s, p);   \
-    else if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p); \
+    if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
     else if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2, 0, true>), grid, \
                                                    block, 0, s, p);                                         \
     else if (v == 2) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2>), grid, block, 0, s, p); \

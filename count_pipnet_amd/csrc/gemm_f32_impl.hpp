@@ -437,8 +437,8 @@ PIPNET_DEV void zero_acc(Acc& acc) {
 // ======================================================================================
 // main path: LDS-DMA staging, swizzled rows, pipelined fragments (K % BK == 0)
 // ======================================================================================
-// WGM = waves along M (2: the 4-wave 2x2 workgroup; 4: the 8-wave 4x2 workgroup of the long-K
-// stage-4 GEMMs, gemm_f32.hip variant 4 -- same wave tile, same K order, bitwise the 4-wave rows)
+// WGM = waves along M (2: the product's 4-wave 2x2 workgroup; 4: an 8-wave 4x2 workgroup -- same wave
+// tile, same K order -- lab only: +4-8 % on the stage-4 GEMMs standalone, nothing inside C2)
 template <int BK, int TM, int WGM = 2>
 struct Geo {
   static constexpr int NW = 2 * WGM;                      // waves per workgroup
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(NTHREADS, MINB) void gemm_f32_tn_kernel(GemmParams 
 }
 
 // 8-wave form (WGM = 4): a (128 TM) x 128 tile, waves 4 (M) x 2 (N) of the same (32 TM) x 64 wave
-// tile (product variant 4; tuning lab tools/gemm_lab.hip variants 60+)
+// tile (tuning lab tools/gemm_lab.hip variants 60+; not dispatched by the product)
 template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS, int ABL = 0, int SH = 0>
 __global__ __launch_bounds__(512, MINB) void gemm_f32_tn8_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM, 4>::TILE_FLOATS];

@@ -54,8 +54,6 @@ def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
         return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if v == 0:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
-    if v == 4:
-        return f"pipnet_gemm::gemm_f32_tn8_kernel<32, 2, {epilogue}, {aload}, 1, 2, 0, 0>"
     if v == 3:
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
     npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped

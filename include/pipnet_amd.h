@@ -342,7 +342,7 @@ int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e,
 
 /* fp32 GEMM variant plan: the variant pipnet_linear_f32 (and the conv / rowscale forms) launch for an
  * M x N x K product with dense 16-B aligned operands -- 0 K-tail kernel, 1 BK16 128-row, 2 BK32
- * 64-row, 3 BK32 128-row, 4 BK32 256-row on 8 waves -- or -PIPNET_ERR_ARG (profiling labels). */
+ * 64-row, 3 BK32 128-row -- or -PIPNET_ERR_ARG (profiling labels). */
 int pipnet_linear_f32_plan(int M, int N, int K);
 
 /* bf16 conv tile plan: the tile id pipnet_conv2d_nhwc_bf16_tile takes for this shape / epilogue

@@ -388,54 +388,6 @@ def test_gemm_product_tile_vs_fp64(gpu, m, n, k, epi):
     assert (buf[:m].double() - ref).abs().max().item() < 1e-3
 
 
-@pytest.mark.parametrize("n,k,epi,aload", [
-    (3072, 768, "gelu", 0),              # stage-4 fc1
-    (768, 3072, "resid", 0),             # stage-4 fc2 (in place)
-    (768, 1536, "bias", 1),              # stage-3 -> 4 downsample (2x2 stride-2 gather)
-])
-def test_gemm_8wave_rows_equal_4wave_rows(gpu, n, k, epi, aload):
-    """Variant 4 (the 8-wave 256-row workgroup) is picked by shape (enough 256-row tiles to fill the
-    chip), variant 3 (the 4-wave 128-row one) below that; both run the same wave tile over the same
-    K order, so a row's bits never depend on which one the batch size selected."""
-    e = {"gelu": _lib.EPI_BIAS_GELU, "resid": _lib.EPI_RESID, "bias": _lib.EPI_BIAS}[epi]
-    g = torch.Generator(device=gpu).manual_seed(n + k)
-    w = torch.randn(n, k, device=gpu, generator=g) * 0.05
-    b = torch.randn(n, device=gpu, generator=g)
-    s = torch.randn(n, device=gpu, generator=g)
-    if aload:                                             # 27 x 27 -> 26 x 26, stride 1 (C2's stage-4 entry)
-        c = k // 4
-        imgs, small = 64, 15
-        x = torch.randn(imgs, 27, 27, c, device=gpu, generator=g)
-        wk = w.view(n, 2, 2, c).contiguous()
-        assert K.gemm_variant(imgs * 676, n, k) == 4 and K.gemm_variant(small * 676, n, k) == 3
-        full = K.conv2x2(x, wk, b, 1)
-        part = K.conv2x2(x[:small].contiguous(), wk, b, 1)
-        torch.cuda.synchronize()
-        assert torch.equal(part, full[:small])
-        ref = torch.nn.functional.conv2d(x[:1].permute(0, 3, 1, 2).double(), wk.permute(0, 3, 1, 2).double(),
-                                         b.double()).permute(0, 2, 3, 1)
-        assert (full[:1].double() - ref).abs().max().item() < 1e-3
-        return
-    m = 43264
-    ms = 10752                                            # 42 x 6 = 252 256-row tiles: variant 3
-    assert K.gemm_variant(m, n, k) == 4 and K.gemm_variant(ms, n, k) == 3
-    a = torch.randn(m, k, device=gpu, generator=g)
-    r = torch.randn(m, n, device=gpu, generator=g)
-    full, part = r.clone(), r[:ms].clone()
-    if epi == "resid":
-        K.linear(a, w, b, e, scale=s, r=full, out=full)
-        K.linear(a[:ms].contiguous(), w, b, e, scale=s, r=part, out=part)
-    else:
-        full = K.linear(a, w, b, e, scale=s)
-        part = K.linear(a[:ms].contiguous(), w, b, e, scale=s)
-    torch.cuda.synchronize()
-    assert torch.equal(part, full[:ms])
-    ref = a[:512].double() @ w.double().t()
-    ref = (torch.nn.functional.gelu(ref + b.double()) if epi == "gelu"
-           else r[:512].double() + s.double() * (ref + b.double()))
-    assert (full[:512].double() - ref).abs().max().item() < 1e-3
-
-
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("b,hw,p,k,thresh", [
     (64, 26 * 26, 768, 200, 0.1),     # C2 head (inference: 0.1 presence threshold)

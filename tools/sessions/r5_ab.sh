@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5: end-to-end A/B of library builds (product vs tools/ab/libpipnet_<arm>.so) on one BASELINE config,
-# interleaved rounds of separate processes.  ARMS="product before" CFG=c3 ROUNDS=3 [LAYERS=l3.c3,l4.c3]
+# interleaved rounds of separate processes.  ARMS="product before" CFG=c3 ROUNDS=3 [LAYERS=l3.c3,l4.c3] [EXTRA="--stream-split 1"]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 R=$PWD
@@ -11,7 +11,7 @@ out=gpurun_out/ab_${CFG}.txt
 lib_of() { if [ $1 = product ]; then echo $R/count_pipnet_amd/libpipnet_amd.so; else echo $R/tools/ab/libpipnet_$1.so; fi; }
 for r in $(seq $ROUNDS); do
   for v in $ARMS; do
-    PIPNET_AMD_ALLOW_STALE=1 PIPNET_AMD_LIB=$(lib_of $v) timeout -k 10 180 python tools/bench_configs.py --only $CFG --steps 20 > gpurun_out/ab_${CFG}_$v.log 2>&1
+    PIPNET_AMD_ALLOW_STALE=1 PIPNET_AMD_LIB=$(lib_of $v) timeout -k 10 180 python tools/bench_configs.py --only $CFG --steps 20 ${EXTRA:-} > gpurun_out/ab_${CFG}_$v.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$CFG arm $v failed rc=$rc" >> $out; tail -5 gpurun_out/ab_${CFG}_$v.log >> $out; exit $rc; }
     echo "$CFG round $r $v $(grep '^{' gpurun_out/ab_${CFG}_$v.log | head -1 | cut -c1-100)" >> $out
   done
