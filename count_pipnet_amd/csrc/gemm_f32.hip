@@ -41,6 +41,7 @@ int gemm_variant(int M, int N, int K, bool vec) {
   // four full rounds of 2 per CU instead of 4,096 64-row tiles in 5.3 rounds of 3; C5 +0.8 % in
   // four interleaved rounds (profiles/r05/ab_c5_addon_tile.txt).  Same K order: bitwise equal.
   if (N >= 1024 && N % BN == 0 && K <= 192 && M > 64) return 3;
+  if (PIPNET_AB_GEMM_RULE == 5 && N == 384 && K >= 768 && M >= 192 * 200) return 5;   // wide 192 x 384 tile
   if (N <= 384 || K <= 192 || M <= 64) return 2;
   return 3;
 }
@@ -102,11 +103,25 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
-  const int v = gemm_variant(p.M, p.N, p.K, vec);
-  p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
-  const dim3 grid(p.mt * p.nt), block(NTHREADS);
+  int v = gemm_variant(p.M, p.N, p.K, vec);
+  // the wide tile: float4 epilogue only, no 3x3 gather / GELU-backward instantiation (their extra
+  // live registers spill at 3 waves per SIMD) -- those fall back to the 64-row tile
+  if (v == 5 && (ALOAD == ALOAD_CONV || epi == PIPNET_EPI_GELU_BWD || !p.vec_epi)) v = 2;
+  if (v == 5) {
+    p.nt = 1;
+    p.mt = (p.M + 191) / 192;
+  } else {
+    p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
+  }
+  const dim3 grid(p.mt * p.nt), block(v == 5 ? 768 : NTHREADS);
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
+    if constexpr (PIPNET_AB_GEMM_RULE == 5 && ALOAD != ALOAD_CONV && E != PIPNET_EPI_GELU_BWD) {           \
+      if (v == 5) {                                                                                       \
+        hipLaunchKernelGGL((gemm_f32_tnw_kernel<E, ALOAD>), grid, block, 0, s, p);                        \
+        break;                                                                                            \
+      }                                                                                                   \
+    }                                                                                                     \
     if (v == 1) hipLaunchKernelGGL((gemm_f32_tn_kernel<16, 2, E, ALOAD, 2, 3>), grid, block, 0, s, p);    \
     else if (v == 2 && p.N % BN) hipLaunchKernelGGL((gemm_f32_tn_kernel<32, 1, E, ALOAD, 3, 2, 0, true>), grid, \
                                                    block, 0, s, p);                                         \

@@ -201,11 +201,16 @@ PIPNET_DEV float gelu_sc16(float x) {
   return fmaf(-ahx, __builtin_amdgcn_rcpf(p), hx + ahx);
 }
 
-using Acc = f32x16[2][2];
+// accumulators of a (32 TM) x 64 wave tile: acc[i][j] = 32 x 32 block (rows i*32.., cols j*32..);
+// TM <= 2 keep the [2][2] shape (TM 1 leaves row 1 unused), TM 3 = the wide tile's 96-row waves
+template <int TM>
+using AccM = f32x16[TM < 2 ? 2 : TM][2];
+using Acc = AccM<2>;
 
 // scalar epilogue (any N / ldc): lane owns column n, rows (v&3) + 8(v>>2) + 4h per tile
-template <int EPI, int TM>
-PIPNET_DEV void epilogue(const GemmParams& p, const Acc& acc, int m0, int n0, int wm, int wn, int lr, int lh) {
+template <int EPI, int TM, int R>
+PIPNET_DEV void epilogue(const GemmParams& p, const f32x16 (&acc)[R][2], int m0, int n0, int wm, int wn, int lr,
+                         int lh) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + j * 32 + lr;
@@ -272,7 +277,8 @@ PIPNET_DEV void epilogue(const GemmParams& p, const Acc16& acc, int m0, int n0, 
 }
 
 // 32-row slab i of a wave's accumulators -> its 32 x 64 LDS image (row-major), per MFMA layout
-PIPNET_DEV void slab_write(float* wt, const Acc& acc, int i, int lane) {
+template <int R>
+PIPNET_DEV void slab_write(float* wt, const f32x16 (&acc)[R][2], int i, int lane) {
   const int lr = lane & 31, lh = lane >> 5;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -358,8 +364,12 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
   // Row addresses as running pointers (+4 rows per step; the residual's clamped rows by a
   // select): a per-access (int64) m * ld is three quarter-rate integer multiplies per store.
   const int mrow0 = m0 + wm * 32 * TM + (lane >> 4);
-  f32x4 r[TM][8];
-  if (HAS_R) {
+  // TM <= 2: every residual float4 of the lane loaded before the first slab (one latency);
+  // TM 3 (96-row waves beside 96 accumulators): one slab's 8 at a time, issued once that slab's
+  // accumulators are in LDS (before the barrier)
+  constexpr bool PRE = TM <= 2;
+  f32x4 r[PRE ? TM : 1][8];
+  if (HAS_R && PRE) {
     const float* rp = p.R + (int64_t)mrow0 * p.ldr + n;
     const float* const rlast = p.R + (int64_t)(p.M - 1) * p.ldr + n;
 #pragma unroll
@@ -376,9 +386,19 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
   for (int i = 0; i < TM; ++i) {
     __syncthreads();
     slab_write(wt, acc, i, lane);
+    if (HAS_R && !PRE) {                  // after the slab's accumulators are dead
+      const float* rp = p.R + (int64_t)(mrow0 + i * 32) * p.ldr + n;
+      const float* const rlast = p.R + (int64_t)(p.M - 1) * p.ldr + n;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const float* src = mrow0 + i * 32 + it * 4 < p.M ? rp : rlast;
+        r[0][it] = nok ? ld4(src) : f32x4{0.f, 0.f, 0.f, 0.f};
+        rp += 4 * p.ldr;
+      }
+    }
     __syncthreads();
     lab_stamp<ABL>(p, 8 + 2 * i);
-    if (i == 0) vm_drain();               // bias / residual preloads landed (common.hpp)
+    if (i == 0 || !PRE) vm_drain();       // bias / residual preloads landed (common.hpp)
     // the slab's 8 LDS reads issued together, outside the row-guarded stores (one latency)
     f32x4 sv[8];
 #pragma unroll
@@ -389,7 +409,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
       const int m = m0 + wm * 32 * TM + i * 32 + row;
       float rs = 1.f;
       if constexpr (EPI == PIPNET_EPI_RESID_ROWSCALE) rs = p.row_scale[min(m, p.M - 1) / p.rows_per_scale];
-      const f32x4 x = epi_math<EPI>(sv[it], bn, sn, HAS_R ? r[i][it] : bn, rs);
+      const f32x4 x = epi_math<EPI>(sv[it], bn, sn, HAS_R ? r[PRE ? i : 0][it] : bn, rs);
       if (m < p.M && nok) st4_c(op, x);
       op += 4 * p.ldc;
       if constexpr ((ABL & 8) != 0) {     // lab: per-iteration timing of the first slab
@@ -406,7 +426,7 @@ PIPNET_DEV void epilogue_vec(const GemmParams& p, const AccT& acc, float* smem, 
 // XCD-contiguous tile ranges, group_m-grouped raster (m fastest inside a group).  (An
 // XCD-slab raster -- each XCD owning an N slab so its W panels stay L2-resident -- measured no
 // faster, profiles/r02/gemm_raster_store_ab.txt.)
-PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
+PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0, int bn = BN) {
   const int nwg = p.mt * p.nt;
   const int tile = xcd_remap(blockIdx.x, nwg);
   const int gm = p.group_m;
@@ -415,7 +435,7 @@ PIPNET_DEV void tile_coords(const GemmParams& p, int bm, int& m0, int& n0) {
   const int gsz = min(p.mt - first_m, gm);
   const int in_group = tile - group * gm * p.nt;
   m0 = (first_m + in_group % gsz) * bm;
-  n0 = (in_group / gsz) * BN;
+  n0 = (in_group / gsz) * bn;
 }
 
 PIPNET_DEV void zero_acc(Acc16& acc) {
@@ -425,9 +445,10 @@ PIPNET_DEV void zero_acc(Acc16& acc) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 }
 
-PIPNET_DEV void zero_acc(Acc& acc) {
+template <int R>
+PIPNET_DEV void zero_acc(f32x16 (&acc)[R][2]) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < R; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -439,15 +460,18 @@ PIPNET_DEV void zero_acc(Acc& acc) {
 // ======================================================================================
 // WGM = waves along M (2: the product's 4-wave 2x2 workgroup; 4: an 8-wave 4x2 workgroup -- same wave
 // tile, same K order -- lab only: +4-8 % on the stage-4 GEMMs standalone, nothing inside C2)
-template <int BK, int TM, int WGM = 2>
+// WGN = waves along N (2: 128 columns; 6: the wide tile's 384 columns, gemm_f32_tnw_kernel)
+template <int BK, int TM, int WGM = 2, int WGN = 2>
 struct Geo {
-  static constexpr int NW = 2 * WGM;                      // waves per workgroup
+  static constexpr int NW = WGM * WGN;                    // waves per workgroup
   static constexpr int BMT = 32 * TM * WGM;               // tile rows of A
+  static constexpr int BNT = 64 * WGN;                    // tile rows of W (output columns)
   static constexpr int CHUNKS = BK / 4;                   // 16-B chunks per LDS row
   static constexpr int ROWS_PER_DMA = 64 / CHUNKS;        // rows one 1-KiB DMA fills
   static constexpr int A_DMA = BMT / ROWS_PER_DMA / NW;
-  static constexpr int B_DMA = BN / ROWS_PER_DMA / NW;
-  static constexpr int TILE_FLOATS = (BMT + BN) * BK;     // one buffer: A rows then B rows
+  static constexpr int B_DMA = BNT / ROWS_PER_DMA / NW;
+  static constexpr int TILE_FLOATS = (BMT + BNT) * BK;    // one buffer: A rows then B rows
+  static_assert(A_DMA * ROWS_PER_DMA * NW == BMT && B_DMA * ROWS_PER_DMA * NW == BNT, "DMA rows per wave");
   static constexpr int NGROUPS = BK / 8;                  // 4-deep fragment groups per half-wave
   // chunk swizzle: the 16 lanes of a ds_read_b128 group read 16 distinct bank slots
   static PIPNET_DEV int swz(int row, int c) {
@@ -455,13 +479,15 @@ struct Geo {
   }
 };
 
-struct Frag {
-  f32x4 a[2], b[2];
+template <int TM>
+struct FragM {
+  f32x4 a[TM < 2 ? 2 : TM], b[2];
 };
+using Frag = FragM<2>;
 
-template <int BK, int TM, int WGM = 2>
-PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int lh, int q) {
-  using G = Geo<BK, TM, WGM>;
+template <int BK, int TM, int WGM = 2, int WGN = 2, class F>
+PIPNET_DEV void read_frag(F& f, const float* buf, int wm, int wn, int lr, int lh, int q) {
+  using G = Geo<BK, TM, WGM, WGN>;
   const int c = lh * (G::CHUNKS / 2) + q;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -477,8 +503,8 @@ PIPNET_DEV void read_frag(Frag& f, const float* buf, int wm, int wn, int lr, int
 
 // JL = how many of the wave's two 32-column blocks take part (2 everywhere except NPAD
 // waves whose blocks lie past N); a compile-time count, so the MFMA stream stays branch-free.
-template <int TM, int JL = 2>
-PIPNET_DEV void mfma_frag(Acc& acc, const Frag& f) {
+template <int TM, int JL = 2, int R, class F>
+PIPNET_DEV void mfma_frag(f32x16 (&acc)[R][2], const F& f) {
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
@@ -552,9 +578,11 @@ PIPNET_DEV void wait_dma_barrier() {
 // workgroups land on different SIMDs (a relabelling: every output is computed identically).
 // SH = MFMA shape: 0 = v_mfma_f32_32x32x2_f32, 1 = v_mfma_f32_16x16x4_f32 (same tile, LDS image,
 // DMA and fragment bytes; a different k order inside each K-tile, so a different rounding).
-template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD, int WGM = 2>
+template <int SH, int BK, int TM, int EPI, int ALOAD, int NS, int ABL, bool NPAD, int WGM = 2, int WGN = 2>
 PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
-  using G = Geo<BK, TM, WGM>;
+  using G = Geo<BK, TM, WGM, WGN>;
+  static_assert(!NPAD || WGN == 2, "NPAD column flip: two waves along N");
+  static_assert(SH == 0 || TM <= 2, "16x16x4 accumulators: TM <= 2");
   constexpr int NWAVES = G::NW;
   static_assert(SH == 0 || BK == 32, "16x16x4 fragments: BK 32 (the swizzle is conflict-free there)");
   // split-K: workgroup row y reduces K-tiles [y*nk/S, (y+1)*nk/S) into its own C slab
@@ -568,10 +596,10 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wid = tid >> 6;
-  const int wm = wid >> 1, wn = NPAD ? ((wid & 1) ^ (int)(blockIdx.x & 1)) : (wid & 1);
+  const int wm = wid / WGN, wn = NPAD ? ((wid & 1) ^ (int)(blockIdx.x & 1)) : wid % WGN;
   const int lr = lane & 31, lh = lane >> 5;
   int m0, n0;
-  tile_coords(p, G::BMT, m0, n0);
+  tile_coords(p, G::BMT, m0, n0, G::BNT);
   const int jl = NPAD ? __builtin_amdgcn_readfirstlane(min(2, max(0, (p.N - n0 - wn * 64 + 31) >> 5))) : 2;
   if (p.stagger && (int)blockIdx.x >= p.stagger_lo && (int)blockIdx.x < p.stagger_hi)
     for (int i = 0; i < p.stagger; ++i) __builtin_amdgcn_s_sleep(127);
@@ -643,7 +671,7 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
     }
   };
 
-  using AccT = typename std::conditional<SH == 0, Acc, Acc16>::type;
+  using AccT = typename std::conditional<SH == 0, AccM<TM>, Acc16>::type;
   AccT acc;
   zero_acc(acc);
   lab_stamp<ABL>(p, 0);
@@ -679,8 +707,8 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
       }
       return;
     } else {
-    Frag fa, fb;
-    read_frag<BK, TM, WGM>(fa, smem, wm, wn, lr, lh, 0);
+    FragM<TM> fa, fb;
+    read_frag<BK, TM, WGM, WGN>(fa, smem, wm, wn, lr, lh, 0);
     int cur = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const float* buf = smem + cur * G::TILE_FLOATS;
@@ -691,19 +719,19 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
         issued = kt + NS - 1;
       }
       if constexpr (G::NGROUPS == 4) {
-        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 1);
+        read_frag<BK, TM, WGM, WGN>(fb, buf, wm, wn, lr, lh, 1);
         mfma_frag<TM, JL>(acc, fa);
-        read_frag<BK, TM, WGM>(fa, buf, wm, wn, lr, lh, 2);
+        read_frag<BK, TM, WGM, WGN>(fa, buf, wm, wn, lr, lh, 2);
         mfma_frag<TM, JL>(acc, fb);
-        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 3);
+        read_frag<BK, TM, WGM, WGN>(fb, buf, wm, wn, lr, lh, 3);
         mfma_frag<TM, JL>(acc, fa);
       } else {
-        read_frag<BK, TM, WGM>(fb, buf, wm, wn, lr, lh, 1);
+        read_frag<BK, TM, WGM, WGN>(fb, buf, wm, wn, lr, lh, 1);
         mfma_frag<TM, JL>(acc, fa);
       }
       const int nxt = (cur + 1 == NS) ? 0 : cur + 1;
       if (!(ABL & 4)) wait_tile(kt + 1 < nk ? kt + 1 : issued, issued);   // tile kt+1 landed, tile kt read
-      if (kt + 1 < nk) read_frag<BK, TM, WGM>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
+      if (kt + 1 < nk) read_frag<BK, TM, WGM, WGN>(fa, smem + nxt * G::TILE_FLOATS, wm, wn, lr, lh, 0);
       mfma_frag<TM, JL>(acc, fb);
       cur = nxt;
     }
@@ -721,12 +749,14 @@ PIPNET_DEV void gemm_tn_body(GemmParams p, float* smem) {
     const float* av = reinterpret_cast<const float*>(&acc);
     float t = 0.f;
 #pragma unroll
-    for (int v = 0; v < 64; ++v) t += av[v];
+    for (int v = 0; v < (int)(sizeof(AccT) / sizeof(float)); ++v) t += av[v];
     p.C[(int64_t)blockIdx.x * 64 * NWAVES + tid] = t;
     return;
   }
-  if (p.vec_epi)
+  if (WGN != 2 || p.vec_epi)            // the wide tile is launched for float4 epilogues only
     epilogue_vec<EPI, TM, AccT, ABL>(p, acc, smem, m0, n0, wm, wn, lane, wid);
+  else if constexpr (WGN != 2)
+    return;
   else if constexpr (SH == 0)
     epilogue<EPI, TM>(p, acc, m0, n0, wm, wn, lr, lh);
   else
@@ -749,6 +779,17 @@ template <int BK, int TM, int EPI, int ALOAD, int MINB, int NS, int ABL = 0, int
 __global__ __launch_bounds__(512, MINB) void gemm_f32_tn8_kernel(GemmParams p) {
   __shared__ __attribute__((aligned(16))) float smem[NS * Geo<BK, TM, 4>::TILE_FLOATS];
   gemm_tn_body<SH, BK, TM, EPI, ALOAD, NS, ABL, false, 4>(p, smem);
+}
+
+// Wide form: a 192 x 384 tile on 12 waves, 2 (M) x 6 (N) of a 96 x 64 wave tile (TM 3) -- the whole
+// N of a 384-column product in one workgroup, so each A panel is fetched once, and 243 tiles of
+// C2's stage-3 fc2 (M = 46,656) fill the 256 CUs in one round.  Per 32-deep K-tile: 73.7 KB of
+// LDS-DMA for 4.7 MFLOP (64 flop per staged byte, 2x the 128 x 128 tile).  One workgroup per CU
+// (2 x 72 KiB stages), 3 waves per SIMD.
+template <int EPI, int ALOAD, int ABL = 0>
+__global__ __launch_bounds__(768, 1) void gemm_f32_tnw_kernel(GemmParams p) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * Geo<32, 3, 2, 6>::TILE_FLOATS];
+  gemm_tn_body<0, 32, 3, EPI, ALOAD, 2, ABL, false, 2, 6>(p, smem);
 }
 
 // the same tile on v_mfma_f32_16x16x4_f32
