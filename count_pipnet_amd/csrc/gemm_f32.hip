@@ -22,16 +22,17 @@ int choose_group_m(const GemmParams& p) {
 //   N <= 384 or K <= 192      BK=32,  64-row tiles, 3 workgroups/CU   (+5..+8 %: shallow grids)
 //   or M <= 64
 //   otherwise                 BK=32, 128-row tiles, 2 LDS stages      (stage-3/4 fc1, fc2)
+//   N = 384, K >= 768         BK=32, 192 x 384 tiles, 12 waves        (stage-3 fc2, round 6)
 // 0 = register-staged K-tail kernel, 1 = BK16x128 rows x3 stages, 2 = BK32x64 rows,
-// 3 = BK32x128 rows (exported by pipnet_linear_f32_plan; the profiling labels of
-// count_pipnet_amd/kernels.py:gemm_kernel_name come from it).  An 8-wave 256 x 128 workgroup
+// 3 = BK32x128 rows, 5 = BK32 192 x 384 wide tile on 12 waves (exported by pipnet_linear_f32_plan;
+// the profiling labels of count_pipnet_amd/kernels.py:gemm_kernel_name come from it).  An 8-wave 256 x 128 workgroup
 // (gemm_f32_impl.hpp gemm_f32_tn8_kernel, tools/gemm_lab.hip 60+) beat variant 3 by 4-8 % on the
 // stage-4 shapes in the lab but not inside C2 (profiles/r06/gemm_tn8_ab.txt): not dispatched.
 // (PIPNET_AB_GEMM_RULE: build-time A/B hook for tools/ab_build.py, 0 in the product)
 #ifndef PIPNET_AB_GEMM_RULE
 #define PIPNET_AB_GEMM_RULE 0
 #endif
-int gemm_variant(int M, int N, int K, bool vec) {
+int gemm_variant(int M, int N, int K, bool vec, int epi, int aload, bool vec_epi) {
   if (!vec) return 0;
   if (K % 16 == 0 && K <= 96 && N > 192 && M > 64) return 1;
   if (K % 32) return K % 16 == 0 && M > 64 ? 1 : 0;
@@ -41,7 +42,14 @@ int gemm_variant(int M, int N, int K, bool vec) {
   // four full rounds of 2 per CU instead of 4,096 64-row tiles in 5.3 rounds of 3; C5 +0.8 % in
   // four interleaved rounds (profiles/r05/ab_c5_addon_tile.txt).  Same K order: bitwise equal.
   if (N >= 1024 && N % BN == 0 && K <= 192 && M > 64) return 3;
-  if (PIPNET_AB_GEMM_RULE == 5 && N == 384 && K >= 768 && M >= 192 * 200) return 5;   // wide 192 x 384 tile
+  // 384 columns at K >= 768 (C2's stage-3 fc2 and the stage-2 -> 3 downsample): the wide 192 x 384
+  // tile (gemm_f32_tnw_kernel) -- each A panel fetched once, 243 tiles = one round at 64 images;
+  // s384 fc2 451 -> 424 us (0.776 -> 0.826 of the fp32 peak), C2 +0.9 % (two streams) / +1.7 % (one)
+  // in interleaved rounds (profiles/r06/gemm_wide_ab.txt).  Same wave K order: bitwise the 64-row
+  // tile's rows.  From 100 tiles, so the two-stream sub-batches (23,328 rows) take it as well.
+  if (PIPNET_AB_GEMM_RULE != 6 && N == 384 && K >= 768 && M >= 192 * 100 && epi != PIPNET_EPI_GELU_BWD &&
+      aload != ALOAD_CONV && vec_epi)
+    return 5;
   if (N <= 384 || K <= 192 || M <= 64) return 2;
   return 3;
 }
@@ -103,10 +111,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
               (!p.R || ((p.ldr % 4 == 0) && aligned16(p.R))) && (!p.bias || aligned16(p.bias)) &&
               (!p.scale || aligned16(p.scale));
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
-  int v = gemm_variant(p.M, p.N, p.K, vec);
-  // the wide tile: float4 epilogue only, no 3x3 gather / GELU-backward instantiation (their extra
-  // live registers spill at 3 waves per SIMD) -- those fall back to the 64-row tile
-  if (v == 5 && (ALOAD == ALOAD_CONV || epi == PIPNET_EPI_GELU_BWD || !p.vec_epi)) v = 2;
+  const int v = gemm_variant(p.M, p.N, p.K, vec, epi, ALOAD, p.vec_epi);
   if (v == 5) {
     p.nt = 1;
     p.mt = (p.M + 191) / 192;
@@ -116,7 +121,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   const dim3 grid(p.mt * p.nt), block(v == 5 ? 768 : NTHREADS);
 #define PIPNET_EPI_CASE(E)                                                                                 \
   case E:                                                                                                 \
-    if constexpr (PIPNET_AB_GEMM_RULE == 5 && ALOAD != ALOAD_CONV && E != PIPNET_EPI_GELU_BWD) {           \
+    if constexpr (ALOAD != ALOAD_CONV && E != PIPNET_EPI_GELU_BWD) {                                      \
       if (v == 5) {                                                                                       \
         hipLaunchKernelGGL((gemm_f32_tnw_kernel<E, ALOAD>), grid, block, 0, s, p);                        \
         break;                                                                                            \
@@ -150,9 +155,10 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
 
 // The variant pipnet_linear_f32 / _rowscale / pipnet_conv2x2_f32 / pipnet_conv2d_nhwc_f32 launch for an
 // M x N x K product with dense, unit-stride, 16-B aligned operands (what torch allocations give).
-extern "C" int pipnet_linear_f32_plan(int M, int N, int K) {
-  if (M < 0 || N < 0 || K <= 0) return -PIPNET_ERR_ARG;
-  return gemm_variant(M, N, K, true);
+extern "C" int pipnet_linear_f32_plan(int M, int N, int K, int epilogue, int aload) {
+  if (M < 0 || N < 0 || K <= 0 || aload < ALOAD_DENSE || aload > ALOAD_CONV) return -PIPNET_ERR_ARG;
+  if (epilogue < PIPNET_EPI_NONE || epilogue > PIPNET_EPI_GELU_BWD) return -PIPNET_ERR_ARG;
+  return gemm_variant(M, N, K, true, epilogue, aload, N % 4 == 0);
 }
 
 extern "C" int pipnet_linear_f32(const float* A, int64_t lda, const float* W, const float* bias,

@@ -37,23 +37,25 @@ def _launch(kname: str, flops: float, fn) -> None:
 
 
 @functools.lru_cache(maxsize=4096)
-def gemm_variant(m: int, n: int, k: int) -> int:
+def gemm_variant(m: int, n: int, k: int, epilogue: int = _lib.EPI_NONE, aload: int = 0) -> int:
     """The fp32 GEMM variant the library launches for an m x n x k product (pipnet_linear_f32_plan:
     the library's own rule, csrc/gemm_f32.hip gemm_variant -- never mirrored here)."""
-    v = _lib.load().pipnet_linear_f32_plan(m, n, k)
+    v = _lib.load().pipnet_linear_f32_plan(m, n, k, epilogue, aload)
     if v < 0:
-        raise RuntimeError(f"linear: no GEMM variant for {m} x {n} x {k}")
+        raise RuntimeError(f"linear: no GEMM variant for {m} x {n} x {k} (epilogue {epilogue}, aload {aload})")
     return v
 
 
 def gemm_kernel_name(m: int, n: int, k: int, epilogue: int, aload: int) -> str:
     """The rocprof name of the GEMM instantiation the library picks (dense, unit-stride, 16-B
     aligned torch operands -- so ``vec_epi`` holds whenever N % 4 == 0)."""
-    v = gemm_variant(m, n, k)
+    v = gemm_variant(m, n, k, epilogue, aload)
     if v == 1:
         return f"pipnet_gemm::gemm_f32_tn_kernel<16, 2, {epilogue}, {aload}, 2, 3, 0, false>"
     if v == 0:
         return f"pipnet_gemm::gemm_f32_tn_ktail_kernel<{epilogue}, {aload}>"
+    if v == 5:
+        return f"pipnet_gemm::gemm_f32_tnw_kernel<{epilogue}, {aload}, 0>"
     if v == 3:
         return f"pipnet_gemm::gemm_f32_tn_kernel<32, 2, {epilogue}, {aload}, 2, 2, 0, false>"
     npad = "true" if n % 128 else "false"      # padded-column MFMA blocks skipped

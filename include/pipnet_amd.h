@@ -341,9 +341,11 @@ int pipnet_count_gumbel_devseed_f32(const float* logits, int B, int HW, int P, f
 int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e, float* out, void* stream);
 
 /* fp32 GEMM variant plan: the variant pipnet_linear_f32 (and the conv / rowscale forms) launch for an
- * M x N x K product with dense 16-B aligned operands -- 0 K-tail kernel, 1 BK16 128-row, 2 BK32
- * 64-row, 3 BK32 128-row -- or -PIPNET_ERR_ARG (profiling labels). */
-int pipnet_linear_f32_plan(int M, int N, int K);
+ * M x N x K product with dense 16-B aligned operands, PIPNET_EPI_* epilogue and A-operand gather
+ * (0 dense / linear, 1 the 2x2 patch conv, 2 the general NHWC conv) -- 0 K-tail kernel, 1 BK16
+ * 128-row, 2 BK32 64-row, 3 BK32 128-row, 5 BK32 192 x 384 on 12 waves -- or -PIPNET_ERR_ARG
+ * (profiling labels). */
+int pipnet_linear_f32_plan(int M, int N, int K, int epilogue, int aload);
 
 /* bf16 conv tile plan: the tile id pipnet_conv2d_nhwc_bf16_tile takes for this shape / epilogue
  * (tile -1 = the automatic choice, >= 0 validated), or -PIPNET_ERR_ARG.  The library's own rule,

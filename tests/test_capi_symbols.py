@@ -96,8 +96,14 @@ def test_roofline_kernel_names_exist_in_library():
         name = K.gemm_kernel_name(m, n, k, epi, aload)
         assert name in syms, (m, n, k, epi, aload, name)
     # the plan is the library's own (pipnet_linear_f32_plan), no Python mirror of gemm_variant
-    assert [K.gemm_variant(*s[:3]) for s in shapes[:8]] == [1, 2, 2, 2, 3, 2, 3, 3]
-    assert K.gemm_variant(300, 256, 512) == 2 and K.gemm_variant(43264, 768, 1536) == 3
+    assert [K.gemm_variant(*s[:4], s[4]) for s in shapes[:8]] == [1, 2, 2, 2, 3, 5, 3, 3]
+    assert K.gemm_variant(300, 256, 512) == 2 and K.gemm_variant(43264, 768, 1536, _lib.EPI_BIAS, 1) == 3
+    # the wide 192 x 384 tile: from 100 tiles (C2's two-stream sub-batches), dense / 2x2 gather only
+    assert K.gemm_variant(23328, 384, 1536, _lib.EPI_RESID) == 5 and K.gemm_variant(19199, 384, 1536) == 2
+    assert K.gemm_variant(46656, 384, 768, _lib.EPI_BIAS, 1) == 5
+    assert K.gemm_variant(46656, 384, 768, _lib.EPI_BIAS, 2) == 2
+    assert K.gemm_variant(46656, 384, 1536, _lib.EPI_GELU_BWD) == 2
+    assert "gemm_f32_tnw_kernel" in K.gemm_kernel_name(46656, 384, 768, _lib.EPI_BIAS, 1)
     # split-bf16 ConvNeXt GEMMs (stage-1/2 fc1 / fc2 incl. the N = 96 padded-column tile) and
     # ResNet bf16 convs
     out = _nm_demangled()

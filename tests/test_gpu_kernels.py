@@ -388,6 +388,61 @@ def test_gemm_product_tile_vs_fp64(gpu, m, n, k, epi):
     assert (buf[:m].double() - ref).abs().max().item() < 1e-3
 
 
+@pytest.mark.parametrize("k,epi,aload", [
+    (1536, "resid", 0),                  # C2 stage-3 fc2 (in place)
+    (768, "bias", 1),                    # stage-2 -> 3 downsample (2x2 stride-1 gather, 28 -> 27)
+    (1536, "none", 0),
+])
+def test_gemm_wide_rows_equal_64row_rows(gpu, k, epi, aload):
+    """Variant 5 (the 192 x 384 tile on 12 waves) is picked by shape (N = 384, K >= 768, >= 100
+    tiles), variant 2 (the 64-row tile) below that; both run the same 32 x 64 wave K order, so a
+    row's bits never depend on which one the batch size selected; ragged last tiles stay in bounds."""
+    n = 384
+    e = {"resid": _lib.EPI_RESID, "bias": _lib.EPI_BIAS, "none": _lib.EPI_NONE}[epi]
+    g = torch.Generator(device=gpu).manual_seed(k + aload)
+    w = torch.randn(n, k, device=gpu, generator=g) * 0.05
+    b = torch.randn(n, device=gpu, generator=g)
+    s = torch.randn(n, device=gpu, generator=g)
+    if aload:
+        c = k // 4
+        imgs, small = 40, 20                               # 28 x 28 -> 27 x 27: 29,160 / 14,580 rows
+        x = torch.randn(imgs, 28, 28, c, device=gpu, generator=g)
+        wk = w.view(n, 2, 2, c).contiguous()
+        assert K.gemm_variant(imgs * 729, n, k, e, 1) == 5 and K.gemm_variant(small * 729, n, k, e, 1) == 2
+        full = K.conv2x2(x, wk, b, 1)
+        part = K.conv2x2(x[:small].contiguous(), wk, b, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(part, full[:small])
+        ref = torch.nn.functional.conv2d(x[:1].permute(0, 3, 1, 2).double(), wk.permute(0, 3, 1, 2).double(),
+                                         b.double()).permute(0, 2, 3, 1)
+        assert (full[:1].double() - ref).abs().max().item() < 1e-3
+        return
+    m, ms = 46656 - 77, 19199                              # ragged wide tiles / 64-row tiles
+    assert K.gemm_variant(m, n, k, e) == 5 and K.gemm_variant(ms, n, k, e) == 2
+    a = torch.randn(m, k, device=gpu, generator=g)
+    r = torch.randn(m + 5, n, device=gpu, generator=g)
+    r[m:] = 12345.0
+    if epi == "resid":
+        full, part = r.clone(), r[:ms].clone()
+        K.linear(a, w, b, e, scale=s, r=full[:m], out=full[:m])
+        K.linear(a[:ms].contiguous(), w, b, e, scale=s, r=part, out=part)
+        torch.cuda.synchronize()
+        assert torch.all(full[m:] == 12345.0)
+    else:
+        full = torch.full((m + 5, n), 12345.0, device=gpu)
+        K.linear(a, w, b, e, scale=s, out=full[:m])
+        part = K.linear(a[:ms].contiguous(), w, b, e, scale=s)
+        torch.cuda.synchronize()
+        assert torch.all(full[m:] == 12345.0)
+    assert torch.equal(part, full[:ms])
+    ref = a[-300:].double() @ w.double().t()
+    if epi == "resid":
+        ref = r[m - 300:m].double() + s.double() * (ref + b.double())
+    elif epi == "bias":
+        ref = ref + b.double()
+    assert (full[m - 300:m].double() - ref).abs().max().item() < 1e-3
+
+
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("b,hw,p,k,thresh", [
     (64, 26 * 26, 768, 200, 0.1),     # C2 head (inference: 0.1 presence threshold)
