@@ -46,7 +46,9 @@ int gemm_variant(int M, int N, int K, bool vec, int epi, int aload, bool vec_epi
   // tile (gemm_f32_tnw_kernel) -- each A panel fetched once, 243 tiles = one round at 64 images;
   // s384 fc2 451 -> 424 us (0.776 -> 0.826 of the fp32 peak), C2 +0.9 % (two streams) / +1.7 % (one)
   // in interleaved rounds (profiles/r06/gemm_wide_ab.txt).  Same wave K order: bitwise the 64-row
-  // tile's rows.  From 100 tiles, so the two-stream sub-batches (23,328 rows) take it as well.
+  // tile's rows.  From 100 tiles, so the two-stream sub-batches (23,328 rows) take it as well.  On
+  // N = 1536 / 3072 / 768 (s384 fc1, s768 fc1 / fc2) it loses 2-10 % to the 128-row tile: 4 / 8 / 2
+  // column tiles per row band put 3.8 / 7.1 / 1.8 rounds on the CUs (gemm_wide_ab.txt part 4).
   if (PIPNET_AB_GEMM_RULE != 6 && N == 384 && K >= 768 && M >= 192 * 100 && epi != PIPNET_EPI_GELU_BWD &&
       aload != ALOAD_CONV && vec_epi)
     return 5;
@@ -113,7 +115,7 @@ int launch_gemm(GemmParams& p, int epi, hipStream_t s) {
   const bool vec = aligned16(p.A) && aligned16(p.W) && (ALOAD != ALOAD_DENSE || (p.lda & 3) == 0);
   const int v = gemm_variant(p.M, p.N, p.K, vec, epi, ALOAD, p.vec_epi);
   if (v == 5) {
-    p.nt = 1;
+    p.nt = p.N / 384;
     p.mt = (p.M + 191) / 192;
   } else {
     p.mt = (p.M + (v == 2 ? 63 : 127)) / (v == 2 ? 64 : 128);
