@@ -40,6 +40,7 @@ SIGNATURES = {
     "pipnet_conv2d_nhwc_bf16_tile": [P, I32, I32, I32, I32, P, P, I32, I32, I32, I32, I32, P, I32, P, I32, P],
     "pipnet_conv2d_nhwc_bf16_plan": [I32, I32, I32, I32, I32, I32, I32, I32, I32, I32, I32],
     "pipnet_linear_f32_plan": [I32, I32, I32, I32, I32],
+    "pipnet_cnblock_mlp_plan": [I64, I32, I32],
     "pipnet_count_gumbel_soft_f32": [P, I32, I32, I32, F32, P, U64, U64, P, P, P],
     "pipnet_philox_exp1_f32": [U64, U64, I64, I32, P, P],
     "pipnet_nonneg_linear_dx_f32": [P, P, I32, I32, I32, P, P],

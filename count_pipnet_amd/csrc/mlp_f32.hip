@@ -355,6 +355,34 @@ bool pipnet_mlp_lab_variant(int C, const float* t, const float* W1, const float*
 // a pixel's result stays independent of the batch it runs in.
 constexpr int MLP_HS2_MAX_HW = 256;
 
+// Workgroup shapes per M (tools/mlp_lab.py, profiles/r05/mlp_lab.txt; round 5 retuned the
+// two-stream half batches of C2): C = 96 takes 4-wave workgroups from 98,304 pixels (C2 stage 1:
+// 100,352 px 165.9 -> 150.7 us, 200,704 px 285.9 -> 273.8) and 8-wave ones at C5's 65,536
+// (89.3 vs 93.3); C = 192 takes HC = 16 chunks at every M >= 8192 -- the HC = 32 chunks need
+// 101 KiB of LDS, one 4-wave workgroup (one wave per SIMD) per CU: C2's 25,088-pixel stage-2
+// half batch 198.6 -> 162.2 us on (16, 8), C5-sized 16,384 px 101.6 -> 99.4 on (16, 4).  Small M
+// (C1: 16 images of 64^2) gets smaller workgroups so that the grid still covers the CUs.
+// Plan code = HC * 100 + NW * 10 + HS (the instantiation cnblock_mlp_kernel<C, HC, NW, 1, HS>).
+int mlp_plan(int m, int C, int hw) {
+  if (C == 96) {
+    if (m >= 98304) return 3241;       // C2 stage 1
+    if (m >= 65536) return 3281;       // C5 stage 1
+    if (m >= 16384) return 3241;
+    if (m >= 8192) return 3221;
+    return 3211;
+  }
+  if (hw > 0 && hw <= MLP_HS2_MAX_HW) return 1682;   // C5 stage 2
+  if (m >= 24576) return 1681;         // C2 stage 2
+  if (m >= 8192) return 1641;
+  if (m >= 4096) return 3221;
+  return 3211;
+}
+
+extern "C" int pipnet_cnblock_mlp_plan(int64_t M, int C, int hw) {
+  if (M < 0 || M >= ((int64_t)1 << 31) || (C != 96 && C != 192) || hw < 0) return -PIPNET_ERR_ARG;
+  return mlp_plan((int)M, C, hw);
+}
+
 extern "C" int pipnet_cnblock_mlp_hw_f32(const float* t, const float* W1, const float* b1, const float* W2,
                                          const float* b2, const float* gamma, float* x, int64_t M, int C, int hw,
                                          void* stream) {
@@ -368,26 +396,19 @@ extern "C" int pipnet_cnblock_mlp_hw_f32(const float* t, const float* W1, const 
 #ifdef PIPNET_MLP_LAB
   if (pipnet_mlp_lab_variant(C, t, W1, b1, W2, b2, gamma, x, (int)M, s)) return PIPNET_OK;
 #endif
-  // Workgroup shapes per M (tools/mlp_lab.py, profiles/r05/mlp_lab.txt; round 5 retuned the
-  // two-stream half batches of C2): C = 96 takes 4-wave workgroups from 98,304 pixels (C2 stage 1:
-  // 100,352 px 165.9 -> 150.7 us, 200,704 px 285.9 -> 273.8) and 8-wave ones at C5's 65,536
-  // (89.3 vs 93.3); C = 192 takes HC = 16 chunks at every M >= 8192 -- the HC = 32 chunks need
-  // 101 KiB of LDS, one 4-wave workgroup (one wave per SIMD) per CU: C2's 25,088-pixel stage-2
-  // half batch 198.6 -> 162.2 us on (16, 8), C5-sized 16,384 px 101.6 -> 99.4 on (16, 4).  Small M
-  // (C1: 16 images of 64^2) gets smaller workgroups so that the grid still covers the CUs.
   const int m = (int)M;
-  if (C == 96) {
-    if (m >= 98304) return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C2 stage 1
-    if (m >= 65536) return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);     // C5 stage 1
-    if (m >= 16384) return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
-    if (m >= 8192) return launch_mlp<96, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
-    return launch_mlp<96, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+  switch (C * 10000 + mlp_plan(m, C, hw)) {
+    case 963241: return launch_mlp<96, 32, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 963281: return launch_mlp<96, 32, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 963221: return launch_mlp<96, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 963211: return launch_mlp<96, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 1921682: return launch_mlp<192, 16, 8, 1, 2>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 1921681: return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 1921641: return launch_mlp<192, 16, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 1923221: return launch_mlp<192, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    case 1923211: return launch_mlp<192, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
+    default: return PIPNET_ERR_ARG;
   }
-  if (hw > 0 && hw <= MLP_HS2_MAX_HW) return launch_mlp<192, 16, 8, 1, 2>(t, W1, b1, W2, b2, gamma, x, m, s);  // C5 stage 2
-  if (m >= 24576) return launch_mlp<192, 16, 8, 1>(t, W1, b1, W2, b2, gamma, x, m, s);      // C2 stage 2
-  if (m >= 8192) return launch_mlp<192, 16, 4, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
-  if (m >= 4096) return launch_mlp<192, 32, 2, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
-  return launch_mlp<192, 32, 1, 1>(t, W1, b1, W2, b2, gamma, x, m, s);
 }
 
 // map size unknown: the HS = 1 instantiations only

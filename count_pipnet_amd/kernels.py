@@ -491,27 +491,15 @@ def convnext_stem(x_nchw: Tensor, w: Tensor, b: Tensor, ln_w: Tensor, ln_b: Tens
 MLP_FUSED_CHANNELS = (96, 192)
 
 
-MLP_HS2_MAX_HW = 256    # C = 192 on maps of <= 16 x 16: hidden split over two waves (csrc/mlp_f32.hip)
-
-
-# pipnet_cnblock_mlp_hw_f32 thresholds (csrc/mlp_f32.hip, round 5: profiles/r05/mlp_lab.txt)
-MLP_C96_NW4_MIN_M = 98304
-MLP_C192_NW8_MIN_M = 24576
-
-
+@functools.lru_cache(maxsize=1024)
 def cnblock_mlp_kernel_name(c: int, m: int = 1 << 20, hw: int = 0) -> str:
-    """rocprof name of the fused MLP instantiation (mirrors pipnet_cnblock_mlp_hw_f32)."""
-    if c == 192 and 0 < hw <= MLP_HS2_MAX_HW:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
-    if c == 96:
-        nw = 4 if m >= MLP_C96_NW4_MIN_M else 8 if m >= 65536 else 4 if m >= 16384 else 2 if m >= 8192 else 1
-        return f"cnblock_mlp_kernel<96, 32, {nw}, 1, 1>"
-    if m >= MLP_C192_NW8_MIN_M:
-        return "cnblock_mlp_kernel<192, 16, 8, 1, 1>"
-    if m >= 8192:
-        return "cnblock_mlp_kernel<192, 16, 4, 1, 1>"
-    nw = 2 if m >= 4096 else 1
-    return f"cnblock_mlp_kernel<192, 32, {nw}, 1, 1>"
+    """rocprof name of the fused MLP instantiation the library launches (pipnet_cnblock_mlp_plan:
+    the library's own rule, csrc/mlp_f32.hip mlp_plan -- never mirrored here)."""
+    code = _lib.load().pipnet_cnblock_mlp_plan(m, c, hw)
+    if code < 0:
+        raise RuntimeError(f"cnblock_mlp: no plan for M = {m}, C = {c}, hw = {hw}")
+    hc, nw, hs = code // 100, code // 10 % 10, code % 10
+    return f"cnblock_mlp_kernel<{c}, {hc}, {nw}, 1, {hs}>"
 
 
 def cnblock_mlp(t: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, gamma: Tensor, x: Tensor,

@@ -54,7 +54,7 @@ extern "C" {
  * mutable library state -- and the one-launch fused head pipnet_softmax_pool_linear_f32 / _bf16
  * (+ _part_floats) and pipnet_matmul2_f64acc_f32 are new (round 5).  A caller built against an older version must not bind this library.
  * Round 6 only ADDS entry points (pipnet_philox_exp1_f32, pipnet_conv2d_nhwc_bf16_plan,
- * pipnet_linear_f32_plan); no signature changed. */
+ * pipnet_linear_f32_plan, pipnet_cnblock_mlp_plan); no signature changed. */
 #define PIPNET_AMD_ABI_VERSION 3
 int pipnet_amd_abi_version(void);
 const char* pipnet_amd_status_string(int status);
@@ -346,6 +346,11 @@ int pipnet_philox_exp1_f32(uint64_t seed, uint64_t offset, int64_t n, int log_e,
  * 128-row, 2 BK32 64-row, 3 BK32 128-row, 5 BK32 192 x 384 on 12 waves -- or -PIPNET_ERR_ARG
  * (profiling labels). */
 int pipnet_linear_f32_plan(int M, int N, int K, int epilogue, int aload);
+
+/* fused CNBlock MLP plan: the instantiation pipnet_cnblock_mlp_hw_f32 launches for M pixels of C
+ * channels on maps of hw pixels per image (0 = unknown), as HC * 100 + NW * 10 + HS
+ * (cnblock_mlp_kernel<C, HC, NW, 1, HS>), or -PIPNET_ERR_ARG (profiling labels). */
+int pipnet_cnblock_mlp_plan(int64_t M, int C, int hw);
 
 /* bf16 conv tile plan: the tile id pipnet_conv2d_nhwc_bf16_tile takes for this shape / epilogue
  * (tile -1 = the automatic choice, >= 0 validated), or -PIPNET_ERR_ARG.  The library's own rule,

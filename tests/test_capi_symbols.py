@@ -111,6 +111,12 @@ def test_roofline_kernel_names_exist_in_library():
                  (192, 1024)]:                                 # fused narrow-stage MLP (csrc/mlp_f32.hip)
         assert K.cnblock_mlp_kernel_name(c, m) in out, (c, m)
     assert K.cnblock_mlp_kernel_name(192, 16384, hw=256) in out          # hidden split (C5 stage 2)
+    # the labels are the library's plan (pipnet_cnblock_mlp_plan), not a Python mirror
+    assert K.cnblock_mlp_kernel_name(96, 200704) == "cnblock_mlp_kernel<96, 32, 4, 1, 1>"      # C2 stage 1
+    assert K.cnblock_mlp_kernel_name(96, 65536) == "cnblock_mlp_kernel<96, 32, 8, 1, 1>"       # C5 stage 1
+    assert K.cnblock_mlp_kernel_name(192, 25088) == "cnblock_mlp_kernel<192, 16, 8, 1, 1>"     # C2 stage 2 (half)
+    assert K.cnblock_mlp_kernel_name(192, 16384, hw=256) == "cnblock_mlp_kernel<192, 16, 8, 1, 2>"
+    assert K.cnblock_mlp_kernel_name(192, 16384) == "cnblock_mlp_kernel<192, 16, 4, 1, 1>"
     assert "pipnet_bf16::conv_bf16_ppp_kernel<12, 8>" in out                  # dual 1x1 (downsample + conv1)
     assert "pipnet_bf16::stem_pool_bf16_kernel" in out                     # fused stem + max-pool
     for m, n, epi in [(200704, 96, _lib.EPI_F32_RESID), (200704, 384, _lib.EPI_S3_GELU),
