@@ -53,9 +53,9 @@ constexpr int PIX_PER_BLOCK = 32;
 //   * no fences: a release fence per workgroup (partial-slab stores + agent-scope release /
 //     acquire, tried first in round 5) wrote back the L2 behind the streaming proto stores 3,200
 //     times per C3 call and tripled the head's time;
-//   * the GEMV keeps nonneg_linear_kernel's arithmetic exactly (per-thread float4 slices, 16
-//     class partials, fmaf order, wave then cross-wave sums), so the fused head is bitwise the
-//     two-kernel path.
+//   * the GEMV runs nonneg_linear_kernel's per-class arithmetic exactly (nonneg_linear_wave: per-lane
+//     float4 slices, fmaf order, one wave_sum), spread over the workgroup's 4 waves without a
+//     barrier, so the fused head is bitwise the two-kernel path.
 constexpr int NN_CLS_PER_BLOCK = 16;
 
 struct HeadLinear {
@@ -72,61 +72,64 @@ struct HeadLinear {
 
 inline int64_t head_part_floats(int B, int HW, int P) { return HW > 0 ? (int64_t)B * P : 0; }
 
-// One row of NonNegLinear: x (P floats, any address space the caller owns) -> out[0..K).
-// Called by all HEAD_THREADS threads of a workgroup; red = [4][16] floats of LDS.
-PIPNET_DEV void nonneg_linear_row(const float* x, int D, const float* __restrict__ W, const float* __restrict__ bias,
-                                  int K, float* __restrict__ outr, float (*red)[NN_CLS_PER_BLOCK]) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int k0 = 0; k0 < K; k0 += NN_CLS_PER_BLOCK) {
-    const int nk = K - k0 < NN_CLS_PER_BLOCK ? K - k0 : NN_CLS_PER_BLOCK;
-    const float* w0 = W + (int64_t)k0 * D;
-    float s[NN_CLS_PER_BLOCK];
+// NonNegLinear classes [k0, k0 + nk) (nk <= NC) of one row, by ONE wave: lane l owns the float4
+// slices c = 4 l + 256 i of the feature dimension (scalars c = l + 64 i when D % 4 != 0), i
+// ascending, and keeps NC class partials (4 fmaf per slice, .x .. .w); one wave_sum per class; lane
+// 0 writes out[k] = sum + bias[k].  A class's arithmetic depends on (D, class) only -- not on NC,
+// on which wave or workgroup runs it, or on the batch -- so the class-block kernel and the fused
+// head's tail give the same bits.  apply_thresh / x_out: the 0.1 presence threshold applied on
+// load and the clamped row stored (x_out != null only for one wave per row).  x: global or LDS.
+// UNR = slices per unrolled step (registers / loads in flight; not the arithmetic).
+template <int NC, int UNR>
+PIPNET_DEV void nonneg_linear_wave(const float* x, int D, const float* __restrict__ W, const float* __restrict__ bias,
+                                   int k0, int nk, float* __restrict__ outr, int apply_thresh, float thresh,
+                                   float* __restrict__ x_out) {
+  const int lane = threadIdx.x & 63;
+  const float* w0 = W + (int64_t)k0 * D;
+  float s[NC];
 #pragma unroll
-    for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) s[j] = 0.f;
-    if ((D & 3) == 0) {
-      for (int c = 4 * threadIdx.x; c < D; c += 4 * HEAD_THREADS) {
-        const f32x4 xv = ld4(x + c);
-        // rows past nk load row nk-1 and are discarded: a load under a per-class branch
-        // made the compiler wait for each one (16 serialised round trips per slice)
+  for (int j = 0; j < NC; ++j) s[j] = 0.f;
+  if ((D & 3) == 0) {
+#pragma unroll UNR
+    for (int c = 4 * lane; c < D; c += 256) {
+      f32x4 xv = ld4(x + c);
+      if (apply_thresh) {
 #pragma unroll
-        for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
-          const f32x4 w = ld4(w0 + (int64_t)(j < nk ? j : nk - 1) * D + c);
-          s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
-          s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
-          s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
-          s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
-        }
+        for (int e = 0; e < 4; ++e) xv[e] = xv[e] < thresh ? 0.f : xv[e];
       }
-    } else {
-      for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
-        const float xv = x[c];
+      if (x_out) st4(x_out + c, xv);
+      // rows past nk load row nk-1 and are discarded: a load under a per-class branch
+      // made the compiler wait for each one (serialised round trips per slice)
 #pragma unroll
-        for (int j = 0; j < NN_CLS_PER_BLOCK; ++j)
-          s[j] = fmaf(xv, fmaxf(w0[(int64_t)(j < nk ? j : nk - 1) * D + c], 0.f), s[j]);
+      for (int j = 0; j < NC; ++j) {
+        const f32x4 w = ld4(w0 + (int64_t)(j < nk ? j : nk - 1) * D + c);
+        s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
+        s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
+        s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
+        s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
       }
     }
+  } else {
+    for (int c = lane; c < D; c += 64) {
+      float xv = x[c];
+      if (apply_thresh && xv < thresh) xv = 0.f;
+      if (x_out) x_out[c] = xv;
 #pragma unroll
-    for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
-      const float t = wave_sum(s[j]);
-      if (lane == 0) red[wv][j] = t;
+      for (int j = 0; j < NC; ++j) s[j] = fmaf(xv, fmaxf(w0[(int64_t)(j < nk ? j : nk - 1) * D + c], 0.f), s[j]);
     }
-    __syncthreads();
-    if (threadIdx.x < nk) {
-      const int k = k0 + threadIdx.x;
-      float t = red[0][threadIdx.x];
+  }
 #pragma unroll
-      for (int w = 1; w < HEAD_THREADS / 64; ++w) t += red[w][threadIdx.x];
-      outr[k] = t + (bias ? bias[k] : 0.f);
-    }
-    __syncthreads();
+  for (int j = 0; j < NC; ++j) {
+    const float t = wave_sum(s[j]);
+    if (lane == 0 && j < nk) outr[k0 + j] = t + (bias ? bias[k0 + j] : 0.f);
   }
 }
 
 // The fused head's tail, called after the workgroup's atomicMax loop into hl.part.  xs = >= P
 // floats of LDS the workgroup no longer needs.
+template <int TAIL_NC>
 PIPNET_DEV void head_linear_tail(const HeadLinear& hl, int b, int P, float* pooled, float* xs) {
   __shared__ int is_last;
-  __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
   vm_drain();                                  // this thread's atomicMax ops performed
   __syncthreads();
   if (threadIdx.x == 0) is_last = atomicAdd(hl.tickets + b, 1) == (int)gridDim.x - 1;
@@ -142,7 +145,15 @@ PIPNET_DEV void head_linear_tail(const HeadLinear& hl, int b, int P, float* pool
   }
   __syncthreads();
   if (threadIdx.x == 0) atomicExch(hl.tickets + b, 0);   // every workgroup of b has drawn
-  nonneg_linear_row(xs, P, hl.W, hl.bias, hl.K, hl.out + (int64_t)b * hl.K, red);
+  // the GEMV spread over the 4 waves: wave w takes class groups w, w + 4, ... of TAIL_NC classes,
+  // each wave on its own (no barrier) -- K = 200: 13 / 7 groups (TAIL_NC 4 / 8) on the longest wave
+  // instead of 13 workgroup-wide passes with two barriers each.  One slice per step, TAIL_NC per
+  // kernel so that the tail's registers stay under the streaming loop's (a kernel is allocated for
+  // its maximum): fp32 logits 4 (59 VGPRs, the two-kernel head's 55), bf16 quads 8 (118, unchanged).
+  const int wv = threadIdx.x >> 6;
+  for (int k0 = wv * TAIL_NC; k0 < hl.K; k0 += (HEAD_THREADS / 64) * TAIL_NC)
+    nonneg_linear_wave<TAIL_NC, 1>(xs, P, hl.W, hl.bias, k0, min(TAIL_NC, hl.K - k0), hl.out + (int64_t)b * hl.K, 0,
+                                   0.f, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_kernel(const T* __r
     else
       atomicAdd(dst, r);
   }
-  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
+  if constexpr (LIN) head_linear_tail<4>(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
 }
 
 // bf16 logits (the C3 ResNet build, P = 2048), quad layout (round 4): lane l holds channels
@@ -294,15 +305,14 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
     else
       atomicAdd(dst, r);
   }
-  if constexpr (LIN) head_linear_tail(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
+  if constexpr (LIN) head_linear_tail<8>(hl, b, P, pooled, &red[0][0]);   // (its barriers guard red's reuse)
 }
 
 // ---------------------------------------------------------------------------------------
-// NonNegLinear: grid (image, class block of 16).  Every thread owns a float4 slice of the
-// feature dimension (c = 4*tid, 4*tid + 1024, ...) and keeps 16 class partials, so one pass
-// over x issues 16 independent float4 W loads per slice (C5: D = 6144, K = 9 -> 6 slices x 9
-// loads in flight per thread; C2: D = 768, K = 200 -> 13 blocks per image).  Partials are
-// reduced wave-wise then across the 4 waves in a fixed order (batch-invariant).
+// NonNegLinear: grid (image, class block of 16), one wave per 4 classes (nonneg_linear_wave): a
+// lane owns the float4 slices 4 l + 256 i and keeps 4 class partials, two slices per unrolled step
+// (C5: D = 6144, K = 9 -> 24 slices; C2: D = 768, K = 200 -> 13 blocks of 4 waves per image).  No
+// cross-wave reduction: a class's sum is one wave's (batch-invariant, and the fused head's bits).
 // ---------------------------------------------------------------------------------------
 __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float* __restrict__ x, int D,
                                                                      const float* __restrict__ W,
@@ -310,57 +320,12 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
                                                                      int apply_thresh, float thresh,
                                                                      float* __restrict__ x_out,
                                                                      float* __restrict__ out) {
-  __shared__ float red[HEAD_THREADS / 64][NN_CLS_PER_BLOCK];
-  const int b = blockIdx.x, k0 = blockIdx.y * NN_CLS_PER_BLOCK;
-  const int nk = K - k0 < NN_CLS_PER_BLOCK ? K - k0 : NN_CLS_PER_BLOCK;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const float* xr = x + (int64_t)b * D;
-  const float* w0 = W + (int64_t)k0 * D;
-  float s[NN_CLS_PER_BLOCK];
-#pragma unroll
-  for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) s[j] = 0.f;
-  if ((D & 3) == 0) {
-    for (int c = 4 * threadIdx.x; c < D; c += 4 * HEAD_THREADS) {
-      f32x4 xv = ld4(xr + c);
-      if (apply_thresh) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xv[e] = xv[e] < thresh ? 0.f : xv[e];
-      }
-      if (x_out && blockIdx.y == 0) st4(x_out + (int64_t)b * D + c, xv);
-      // rows past nk load row nk-1 and are discarded: a load under a per-class branch
-      // made the compiler wait for each one (16 serialised round trips per slice)
-#pragma unroll
-      for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
-        const f32x4 w = ld4(w0 + (int64_t)(j < nk ? j : nk - 1) * D + c);
-        s[j] = fmaf(xv[0], fmaxf(w[0], 0.f), s[j]);
-        s[j] = fmaf(xv[1], fmaxf(w[1], 0.f), s[j]);
-        s[j] = fmaf(xv[2], fmaxf(w[2], 0.f), s[j]);
-        s[j] = fmaf(xv[3], fmaxf(w[3], 0.f), s[j]);
-      }
-    }
-  } else {
-    for (int c = threadIdx.x; c < D; c += HEAD_THREADS) {
-      float xv = xr[c];
-      if (apply_thresh && xv < thresh) xv = 0.f;
-      if (x_out && blockIdx.y == 0) x_out[(int64_t)b * D + c] = xv;
-#pragma unroll
-      for (int j = 0; j < NN_CLS_PER_BLOCK; ++j)
-        s[j] = fmaf(xv, fmaxf(w0[(int64_t)(j < nk ? j : nk - 1) * D + c], 0.f), s[j]);
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NN_CLS_PER_BLOCK; ++j) {
-    const float t = wave_sum(s[j]);
-    if (lane == 0) red[wv][j] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x < nk) {
-    const int k = k0 + threadIdx.x;
-    float t = red[0][threadIdx.x];
-#pragma unroll
-    for (int w = 1; w < HEAD_THREADS / 64; ++w) t += red[w][threadIdx.x];
-    out[(int64_t)b * K + k] = t + (bias ? bias[k] : 0.f);
-  }
+  constexpr int NCW = NN_CLS_PER_BLOCK / (HEAD_THREADS / 64);     // 4 classes per wave
+  const int b = blockIdx.x, wv = threadIdx.x >> 6;
+  const int k0 = blockIdx.y * NN_CLS_PER_BLOCK + wv * NCW;
+  if (k0 >= K) return;                                             // wave-uniform, no barrier below
+  nonneg_linear_wave<NCW, 2>(x + (int64_t)b * D, D, W, bias, k0, min(NCW, K - k0), out + (int64_t)b * K, apply_thresh,
+                          thresh, (x_out && blockIdx.y == 0 && wv == 0) ? x_out + (int64_t)b * D : nullptr);
 }
 
 // Philox4x32-10 and the Exp(1) / log Exp(1) draws: philox.hpp (shared with the fused add-on
