@@ -310,7 +310,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void softmax_pool_bf16q_kernel(const 
 
 // ---------------------------------------------------------------------------------------
 // NonNegLinear: grid (image, class block of 16), one wave per 4 classes (nonneg_linear_wave): a
-// lane owns the float4 slices 4 l + 256 i and keeps 4 class partials, two slices per unrolled step
+// lane owns the float4 slices 4 l + 256 i and keeps 4 class partials, four slices per unrolled step
 // (C5: D = 6144, K = 9 -> 24 slices; C2: D = 768, K = 200 -> 13 blocks of 4 waves per image).  No
 // cross-wave reduction: a class's sum is one wave's (batch-invariant, and the fused head's bits).
 // ---------------------------------------------------------------------------------------
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(HEAD_THREADS) void nonneg_linear_kernel(const float
   const int b = blockIdx.x, wv = threadIdx.x >> 6;
   const int k0 = blockIdx.y * NN_CLS_PER_BLOCK + wv * NCW;
   if (k0 >= K) return;                                             // wave-uniform, no barrier below
-  nonneg_linear_wave<NCW, 2>(x + (int64_t)b * D, D, W, bias, k0, min(NCW, K - k0), out + (int64_t)b * K, apply_thresh,
+  nonneg_linear_wave<NCW, 4>(x + (int64_t)b * D, D, W, bias, k0, min(NCW, K - k0), out + (int64_t)b * K, apply_thresh,
                           thresh, (x_out && blockIdx.y == 0 && wv == 0) ? x_out + (int64_t)b * D : nullptr);
 }
 
