@@ -391,6 +391,7 @@ def test_gemm_product_tile_vs_fp64(gpu, m, n, k, epi):
 @pytest.mark.parametrize("k,epi,aload", [
     (1536, "resid", 0),                  # C2 stage-3 fc2 (in place)
     (768, "bias", 1),                    # stage-2 -> 3 downsample (2x2 stride-1 gather, 28 -> 27)
+    (768, "bias", 2),                    # torchvision's stride-2 downsample (56 -> 28) at 32 images
     (1536, "none", 0),
 ])
 def test_gemm_wide_rows_equal_64row_rows(gpu, k, epi, aload):
@@ -405,16 +406,20 @@ def test_gemm_wide_rows_equal_64row_rows(gpu, k, epi, aload):
     s = torch.randn(n, device=gpu, generator=g)
     if aload:
         c = k // 4
-        imgs, small = 40, 20                               # 28 x 28 -> 27 x 27: 29,160 / 14,580 rows
-        x = torch.randn(imgs, 28, 28, c, device=gpu, generator=g)
+        stride = aload                 # (the column is the 2x2 gather stride) 1: 28 -> 27 (C2), 2: 56 -> 28
+        hin = 28 if stride == 1 else 56
+        hout = (hin - 2) // stride + 1
+        imgs, small = (40, 20) if stride == 1 else (32, 16)  # 29,160 / 14,580 or 25,088 / 12,544 rows
+        x = torch.randn(imgs, hin, hin, c, device=gpu, generator=g)
         wk = w.view(n, 2, 2, c).contiguous()
-        assert K.gemm_variant(imgs * 729, n, k, e, 1) == 5 and K.gemm_variant(small * 729, n, k, e, 1) == 2
-        full = K.conv2x2(x, wk, b, 1)
-        part = K.conv2x2(x[:small].contiguous(), wk, b, 1)
+        hw = hout * hout
+        assert K.gemm_variant(imgs * hw, n, k, e, 1) == 5 and K.gemm_variant(small * hw, n, k, e, 1) == 2
+        full = K.conv2x2(x, wk, b, stride)
+        part = K.conv2x2(x[:small].contiguous(), wk, b, stride)
         torch.cuda.synchronize()
         assert torch.equal(part, full[:small])
         ref = torch.nn.functional.conv2d(x[:1].permute(0, 3, 1, 2).double(), wk.permute(0, 3, 1, 2).double(),
-                                         b.double()).permute(0, 2, 3, 1)
+                                         b.double(), stride=stride).permute(0, 2, 3, 1)
         assert (full[:1].double() - ref).abs().max().item() < 1e-3
         return
     m, ms = 46656 - 77, 19199                              # ragged wide tiles / 64-row tiles
